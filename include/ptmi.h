@@ -1,0 +1,149 @@
+/*
+ * ptmi.h — C-ABI of libptmi.so, the MI355X (gfx950) path-tracing integrator.
+ *
+ * This is the drop-in boundary for the reference's hot loop: the Taichi
+ * kernels the reference launches directly from its host class
+ * (src/render_server/taichi_renderer/renderer.py) — there is no FFI in the
+ * reference, so each entry point below names the reference launch/host site it
+ * replaces. Plain C types only: device pointers are raw pointers owned by the
+ * caller (the Python host allocates them as torch tensors); the library never
+ * allocates inside a render call. All functions return 0 on success and a
+ * negative PTMI_E* code on error; ptmi_last_error() gives a message.
+ */
+#ifndef PTMI_H
+#define PTMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTMI_ABI_VERSION 1
+#define PTMI_MAX_IMAGES 16
+
+enum {
+    PTMI_OK = 0,
+    PTMI_EINVAL = -1,      /* bad argument / shape */
+    PTMI_ECAPACITY = -2,   /* scene exceeds a structural limit (e.g. BVH depth) */
+    PTMI_EHIP = -3,        /* HIP runtime error */
+    PTMI_ENODEV = -4,      /* no gfx950 device */
+};
+
+/* Device scene, packed by the host from the reference's compiled arrays
+ * (scene_compiler.py:931 compile_scene + bvh_compiler.py:132 compile_bvh;
+ * replaces the field uploads of renderer.py:102-228 / fields.py:25-153).
+ * Layouts (all little-endian, 16-byte aligned):
+ *   nodes   : n_inner x 16 f32 — internal BVH2 node holding BOTH children's
+ *             boxes: {c0.min.xyz, c0.max.x | c0.max.yz, c1.min.xy |
+ *             c1.min.z, c1.max.xyz | ref0, ref1, 0, 0 (as i32 bits)}.
+ *             ref >= 0: internal node index; ref < 0: leaf code
+ *             0x80000000 | type << 28 | prim index (type: 0 sphere,
+ *             1 triangle, 2 quad — scene_compiler.py:10-12).
+ *   spheres : ns x 4 f32 {cx, cy, cz, r}                (fields.py:25)
+ *   quads   : nq x 16 f32 {n.xyz, D | Q.xyz, u.x | u.yz, v.xy | v.z, w.xyz}
+ *   tris    : nt x 12 f32 {v0.xyz, e1.x | e1.yz, e2.xy | e2.z, n.xyz}
+ *   mats    : (ns+nq+nt) x 20 f32, spheres then quads then triangles:
+ *             {albedo.xyz, fuzz | emit.xyz, ir | color1.xyz, tex_scale |
+ *              color2.xyz, density | medium_albedo.xyz, flags(u32 bits)}
+ *             flags = mat_type | tex_type << 4 | is_medium << 8 |
+ *                     (image_index + 1) << 16
+ *   texels  : RGBA8 texels of all image textures, image k at img_offset[k]
+ *   perlin_vec  : 256 x 4 f32 (randvec, w unused)
+ *   perlin_perm : 3 x 256 i32 (perm_x, perm_y, perm_z)
+ */
+typedef struct ptmi_scene_view {
+    const float *nodes;
+    int32_t n_inner;
+    int32_t root_ref;          /* ref of the root (0 if internal) */
+    float root_min[3], root_max[3];
+    int32_t max_leaf_depth;    /* root = 0; sizes the traversal stack */
+    const float *spheres;
+    const float *quads;
+    const float *tris;
+    const float *mats;
+    int32_t num_spheres, num_quads, num_triangles;
+    const uint32_t *texels;
+    int32_t num_images;
+    int32_t img_offset[PTMI_MAX_IMAGES], img_w[PTMI_MAX_IMAGES], img_h[PTMI_MAX_IMAGES];
+    const float *perlin_vec;
+    const int32_t *perlin_perm;
+} ptmi_scene_view;
+
+/* Camera upload values (renderer.py:230-247 / fields.py:159-165). */
+typedef struct ptmi_camera {
+    float center[3], pixel00[3], delta_u[3], delta_v[3], defocus_u[3], defocus_v[3];
+    float defocus_angle;
+} ptmi_camera;
+
+/* One render request: camera + render state (fields.py:171-172) + the pixel
+ * set this call owns. The pixel set is the window [x0,x0+w) x [y0,y0+h)
+ * restricted to rows whose band ((row - y0) / band_rows) satisfies
+ * band % band_stride == band_offset (band_stride = 1: every row). Multi-GPU
+ * tile sharding uses band_stride = world size, band_offset = rank. */
+typedef struct ptmi_frame {
+    ptmi_camera cam;
+    float bg[3];
+    int32_t max_depth;
+    uint32_t seed;
+    int32_t width, height;
+    int32_t x0, y0, w, h;
+    int32_t band_rows, band_stride, band_offset;
+} ptmi_frame;
+
+/* Device counters (u64): [0] ray segments traced from the depth loop / waves,
+ * [1] medium-exit traversals (kernels.py:417), [2] completed paths,
+ * [3] reserved. Accumulated with atomics; pass NULL to skip. */
+#define PTMI_NUM_COUNTERS 4
+
+int ptmi_version(void);
+const char *ptmi_last_error(void);
+
+/* Checks a scene view's counts, alignment and structural limits on the host. */
+int ptmi_scene_check(const ptmi_scene_view *scene);
+
+/* Megakernel: replaces kernels.render_sample() (kernels.py:1177-1202) as
+ * launched by TaichiRenderer.render() (renderer.py:405-409) and
+ * InteractiveViewer (interactive_viewer.py:389): accumulates samples
+ * [sample_begin, sample_begin + sample_count) of every pixel of the frame's
+ * pixel set into accum (height x width x 3 f32, row-major), adding each
+ * sample's colour in sample order. One launch covers many samples (each
+ * thread regenerates its pixel's next path as the previous one ends). */
+int ptmi_mk_render(const ptmi_scene_view *scene, const ptmi_frame *frame, float *accum,
+                   int32_t sample_begin, int32_t sample_count, uint64_t *counters, void *stream);
+
+/* Wavefront: replaces generate_camera_rays / intersect_rays /
+ * shade_miss_rays / reset_next_ray_count / shade_and_scatter /
+ * swap_ray_buffers (kernels.py:1219-1418) as driven by
+ * TaichiRenderer.render_wavefront() (renderer.py:305-334). workspace must be
+ * ptmi_wf_workspace_bytes(frame) bytes of device memory (16-byte aligned). */
+size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame);
+int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
+                   size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
+                   uint64_t *counters, void *stream);
+
+/* Clears the accumulator's pixel set: kernels.clear_accum_buffer()
+ * (kernels.py:1205-1209) / fields.clear_accumulation_buffer (fields.py:280). */
+int ptmi_clear(const ptmi_frame *frame, float *accum, void *stream);
+
+/* Tone map: LivePreview.buffer_to_image (preview.py:117-132):
+ * u8 = clip(sqrt(max(0, accum * (1/max(1,spp)))) * 255.999, 0, 255). */
+int ptmi_tonemap(const float *accum, uint8_t *out, int32_t width, int32_t height, int32_t spp,
+                 void *stream);
+
+/* Host-side binned-SAH BVH build (sah_bvh_builder.py:167-418 via
+ * build_sah_bvh_from_primitives :445-485), f32 arithmetic identical to the
+ * reference under NumPy >= 2 (NEP 50). Inputs (f32): spheres ns x 4
+ * {c.xyz, r}; quads nq x 9 {Q, u, v}; tris nt x 9 {v0, v1, v2}. Outputs are the
+ * 7 flattened arrays, capacity 2*(ns+nq+nt)-1 nodes; *n_nodes receives the
+ * count. */
+int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int32_t nq,
+                       const float *tris, int32_t nt, float *bbox_min, float *bbox_max,
+                       int32_t *left, int32_t *right, int32_t *parent, int32_t *prim_type,
+                       int32_t *prim_idx, int32_t *n_nodes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTMI_H */

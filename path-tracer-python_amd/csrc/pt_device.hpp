@@ -1,0 +1,499 @@
+// pt_device.hpp — gfx950 device-side building blocks of the integrator:
+// packed scene access, primitive intersection, the child-box BVH2 traversal
+// with an LDS stack, textures, materials and the medium step.
+//
+// Semantics follow src/render_server/taichi_renderer/kernels.py (cited per
+// function); arithmetic and random draws follow include/ptmi_math.h and
+// include/ptmi_rng.h so results are bit-identical to the CPU oracle.
+// Compile with -ffp-contract=off (see Makefile).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ptmi.h"
+#include "../../include/ptmi_math.h"
+#include "../../include/ptmi_rng.h"
+
+namespace ptmi {
+
+constexpr float kTMin = 0.001f;     // kernels.py:1057, 1254
+constexpr float kTMax = 1e10f;
+constexpr int kRRMinDepth = 5;      // kernels.py:1050
+constexpr float kRRMaxProb = 0.95f; // kernels.py:1051
+constexpr int kBlock = 256;
+
+enum : int32_t { kSphere = 0, kTriangle = 1, kQuad = 2 };
+
+struct DevScene {
+  const float4* __restrict__ nodes;
+  int32_t n_inner;
+  int32_t root_ref;
+  float root_min[3], root_max[3];
+  const float4* __restrict__ spheres;
+  const float4* __restrict__ quads;
+  const float4* __restrict__ tris;
+  const float4* __restrict__ mats;
+  int32_t mat_base[3];  // indexed by prim type: sphere 0, triangle ns+nq, quad ns
+  const uint32_t* __restrict__ texels;
+  int32_t num_images;
+  int32_t img_offset[PTMI_MAX_IMAGES], img_w[PTMI_MAX_IMAGES], img_h[PTMI_MAX_IMAGES];
+  const float4* __restrict__ perlin_vec;
+  const int32_t* __restrict__ perlin_perm;
+};
+
+struct DevFrame {
+  float center[3], pixel00[3], delta_u[3], delta_v[3], defocus_u[3], defocus_v[3];
+  float defocus_angle;
+  float bg[3];
+  int32_t max_depth;
+  uint32_t seed;
+  int32_t width, height;
+  int32_t x0, y0, w, h;
+  int32_t band_rows, band_stride, band_offset;
+  int32_t n_rows;  // rows of the window this frame owns (after banding)
+};
+
+__device__ __forceinline__ int32_t leaf_type(int32_t ref) { return (ref >> 28) & 3; }
+__device__ __forceinline__ int32_t leaf_index(int32_t ref) { return ref & 0x0fffffff; }
+
+// Local row (0..n_rows-1) -> image row, or -1.
+__device__ __forceinline__ int32_t frame_row(const DevFrame& fr, int32_t lr) {
+  int32_t band = lr / fr.band_rows;
+  int32_t within = lr - band * fr.band_rows;
+  int32_t row = fr.y0 + (band * fr.band_stride + fr.band_offset) * fr.band_rows + within;
+  return (row < fr.y0 + fr.h) ? row : -1;
+}
+
+// ---------------------------------------------------------------- RNG
+struct Rng {
+  uint32_t key, n;
+  __device__ __forceinline__ float next() { return pt_rand(key, n++); }
+};
+
+__device__ __forceinline__ pt_v3 random_in_unit_disk(Rng& r) {  // kernels.py:17-25
+  for (;;) {
+    float x = r.next() * 2.0f - 1.0f;
+    float y = r.next() * 2.0f - 1.0f;
+    pt_v3 p = pt_v3f(x, y, 0.0f);
+    if (pt_dot(p, p) < 1.0f) return p;
+  }
+}
+
+__device__ __forceinline__ pt_v3 random_unit_vector(Rng& r) {  // kernels.py:29-38
+  for (;;) {
+    float x = r.next() * 2.0f - 1.0f;
+    float y = r.next() * 2.0f - 1.0f;
+    float z = r.next() * 2.0f - 1.0f;
+    pt_v3 p = pt_v3f(x, y, z);
+    float l2 = pt_dot(p, p);
+    if (l2 < 1.0f && l2 > 1e-20f) return pt_normalize(p);
+  }
+}
+
+__device__ __forceinline__ pt_v3 random_cosine_direction(pt_v3 n, Rng& r) {  // kernels.py:42-71
+  float r1 = r.next();
+  float r2 = r.next();
+  float z = sqrtf(1.0f - r2);
+  float phi = PT_2PI_F * r1;
+  float st = sqrtf(r2);
+  float sp, cp;
+  pt_sincosf(phi, &sp, &cp);
+  float x = cp * st, y = sp * st;
+  pt_v3 w = pt_normalize(n);
+  pt_v3 a = (fabsf(w.x) < 0.9f) ? pt_v3f(1.0f, 0.0f, 0.0f)
+            : (fabsf(w.y) < 0.9f) ? pt_v3f(0.0f, 1.0f, 0.0f) : pt_v3f(0.0f, 0.0f, 1.0f);
+  pt_v3 v = pt_normalize(pt_cross(a, w));
+  pt_v3 u = pt_cross(v, w);
+  return pt_normalize(pt_add(pt_add(pt_scale(u, x), pt_scale(v, y)), pt_scale(w, z)));
+}
+
+// ---------------------------------------------------------------- camera
+// kernels.py:177-201 (get_ray). Returns the unnormalized direction.
+__device__ __forceinline__ void get_ray(const DevFrame& fr, int32_t px, int32_t py, Rng& r, pt_v3& o,
+                                        pt_v3& d) {
+  float ox = r.next() - 0.5f;
+  float oy = r.next() - 0.5f;
+  pt_v3 p00 = pt_v3f(fr.pixel00[0], fr.pixel00[1], fr.pixel00[2]);
+  pt_v3 du = pt_v3f(fr.delta_u[0], fr.delta_u[1], fr.delta_u[2]);
+  pt_v3 dv = pt_v3f(fr.delta_v[0], fr.delta_v[1], fr.delta_v[2]);
+  pt_v3 ps = pt_add(pt_add(p00, pt_scale(du, (float)px + ox)), pt_scale(dv, (float)py + oy));
+  pt_v3 c = pt_v3f(fr.center[0], fr.center[1], fr.center[2]);
+  o = c;
+  if (fr.defocus_angle > 0.0f) {
+    pt_v3 p = random_in_unit_disk(r);
+    pt_v3 fu = pt_v3f(fr.defocus_u[0], fr.defocus_u[1], fr.defocus_u[2]);
+    pt_v3 fv = pt_v3f(fr.defocus_v[0], fr.defocus_v[1], fr.defocus_v[2]);
+    o = pt_add(pt_add(c, pt_scale(fu, p.x)), pt_scale(fv, p.y));
+  }
+  d = pt_sub(ps, o);
+}
+
+// ---------------------------------------------------------------- primitives
+// Each returns the candidate t (hit only if returned true); hit point and
+// normal are recomputed at shading time from (o, d, t) with the same
+// operation order the reference uses inside the hit functions.
+
+__device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, float tmin, float tmax,
+                                             float& t) {  // kernels.py:209-248
+  pt_v3 c = pt_v3f(s.x, s.y, s.z);
+  pt_v3 oc = pt_sub(c, o);
+  float a = pt_dot(d, d);
+  float h = pt_dot(d, oc);
+  float cc = pt_dot(oc, oc) - s.w * s.w;
+  float disc = h * h - a * cc;
+  if (disc >= 0.0f) {
+    float sq = sqrtf(disc);
+    float root = (h - sq) / a;
+    if (root < tmin || root > tmax) root = (h + sq) / a;
+    if (root >= tmin && root <= tmax) { t = root; return true; }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o, pt_v3 d, float tmin,
+                                           float tmax, float& t) {  // kernels.py:311-362
+  float4 a = q[0], b = q[1], c = q[2], e = q[3];
+  pt_v3 n = pt_v3f(a.x, a.y, a.z);
+  float denom = pt_dot(n, d);
+  if (fabsf(denom) >= 1e-8f) {
+    float tt = (a.w - pt_dot(n, o)) / denom;
+    if (tt >= tmin && tt <= tmax) {
+      pt_v3 Q = pt_v3f(b.x, b.y, b.z), u = pt_v3f(b.w, c.x, c.y), v = pt_v3f(c.z, c.w, e.x);
+      pt_v3 w = pt_v3f(e.y, e.z, e.w);
+      pt_v3 ip = pt_add(o, pt_scale(d, tt));
+      pt_v3 pv = pt_sub(ip, Q);
+      float alpha = pt_dot(w, pt_cross(pv, v));
+      float beta = pt_dot(w, pt_cross(u, pv));
+      if (alpha >= 0.0f && alpha <= 1.0f && beta >= 0.0f && beta <= 1.0f) { t = tt; return true; }
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
+                                          float tmax, float& t) {  // kernels.py:252-307
+  float4 a = tr[0], b = tr[1], c = tr[2];
+  pt_v3 v0 = pt_v3f(a.x, a.y, a.z), e1 = pt_v3f(a.w, b.x, b.y), e2 = pt_v3f(b.z, b.w, c.x);
+  pt_v3 hv = pt_cross(d, e2);
+  float det = pt_dot(e1, hv);
+  if (fabsf(det) >= 1e-8f) {
+    float inv = 1.0f / det;
+    pt_v3 s = pt_sub(o, v0);
+    float u = inv * pt_dot(s, hv);
+    if (u >= 0.0f && u <= 1.0f) {
+      pt_v3 q = pt_cross(s, e1);
+      float v = inv * pt_dot(d, q);
+      if (v >= 0.0f && u + v <= 1.0f) {
+        float tt = inv * pt_dot(e2, q);
+        if (tt >= tmin && tt <= tmax) { t = tt; return true; }
+      }
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool hit_leaf(const DevScene& sc, int32_t ref, pt_v3 o, pt_v3 d, float tmin,
+                                         float tmax, float& t) {
+  int32_t ty = leaf_type(ref), ix = leaf_index(ref);
+  if (ty == kSphere) return hit_sphere_t(sc.spheres[ix], o, d, tmin, tmax, t);
+  if (ty == kQuad) return hit_quad_t(sc.quads + 4 * ix, o, d, tmin, tmax, t);
+  return hit_tri_t(sc.tris + 3 * ix, o, d, tmin, tmax, t);
+}
+
+// Surface normal of a hit, kernels.py:246, 300-305, 355-360.
+__device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_v3 hp, pt_v3 d) {
+  int32_t ty = leaf_type(ref), ix = leaf_index(ref);
+  if (ty == kSphere) {
+    float4 s = sc.spheres[ix];
+    return pt_divs(pt_sub(hp, pt_v3f(s.x, s.y, s.z)), s.w);
+  }
+  if (ty == kQuad) {
+    float4 a = sc.quads[4 * ix];
+    pt_v3 n = pt_v3f(a.x, a.y, a.z);
+    return (pt_dot(n, d) < 0.0f) ? n : pt_neg(n);
+  }
+  float4 c = sc.tris[3 * ix + 2];
+  pt_v3 n = pt_v3f(c.y, c.z, c.w);
+  return (pt_dot(d, n) > 0.0f) ? pt_neg(n) : n;
+}
+
+// ---------------------------------------------------------------- traversal
+// Closest hit over the child-box BVH2 with the reference's visiting order
+// (traverse_bvh_legacy, kernels.py:625-742): far child pushed first by the
+// projected distance of the children's box centres, a popped node culled
+// when its box misses [t_min, closest_t], closest hit updated only when
+// t < closest_t. Each stack entry carries the child's slab entry distance E
+// (computed once when the parent is expanded); the reference's pop-time
+// test max(E, t_min) <= min(X, closest_t) is split exactly into X >= E (at
+// push) and E <= closest_t (at pop). Stack: STACK slots per thread in LDS,
+// slot-major so a wave's 64 lanes hit 64 distinct banks.
+
+struct Stack {
+  uint32_t* ref;  // &lds_ref[tid]
+  float* te;      // &lds_t[tid]
+};
+
+__device__ __forceinline__ void child_slab(float4 lo_a, pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz,
+                                           float mxx, float mxy, float mxz, float tmin, float& E, float& X) {
+  float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
+  float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
+  float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
+  E = pt_maxf(pt_maxf(pt_minf(t0x, t1x), pt_minf(t0y, t1y)), pt_maxf(pt_minf(t0z, t1z), tmin));
+  X = pt_minf(pt_minf(pt_maxf(t0x, t1x), pt_maxf(t0y, t1y)), pt_maxf(t0z, t1z));
+  (void)lo_a;
+}
+
+template <int STACK>
+__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
+                                         Stack st, float& t_out, int32_t& ref_out) {
+  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  float closest = tmax;
+  int32_t best = 0;
+  bool any = false;
+  int sp = 0;
+  if (sc.n_inner == 0 && sc.root_ref >= 0) {  // empty scene
+    t_out = tmax;
+    ref_out = 0;
+    return false;
+  }
+  {
+    float E, X;
+    child_slab(float4(), o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0],
+               sc.root_max[1], sc.root_max[2], tmin, E, X);
+    if (pt_minf(X, closest) >= E) {
+      st.ref[0] = (uint32_t)sc.root_ref;
+      st.te[0] = E;
+      sp = 1;
+    }
+  }
+  while (sp > 0) {
+    --sp;
+    int32_t ref = (int32_t)st.ref[sp * kBlock];
+    float te = st.te[sp * kBlock];
+    if (!(te <= closest)) continue;
+    if (ref < 0) {
+      float t;
+      if (hit_leaf(sc, ref, o, d, tmin, closest, t) && t < closest) {
+        closest = t;
+        best = ref;
+        any = true;
+      }
+      continue;
+    }
+    const float4* nd = sc.nodes + 4 * ref;
+    float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+    int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+    float E0, X0, E1, X1;
+    child_slab(a, o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
+    child_slab(a, o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
+    pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
+    pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
+    float ld = pt_dot(pt_sub(lc, o), d);
+    float rd = pt_dot(pt_sub(rc, o), d);
+    bool h0 = X0 >= E0, h1 = X1 >= E1;
+    // push far first: left nearer -> push right then left
+    int32_t fr = (ld < rd) ? r1 : r0, nr = (ld < rd) ? r0 : r1;
+    float fE = (ld < rd) ? E1 : E0, nE = (ld < rd) ? E0 : E1;
+    bool fh = (ld < rd) ? h1 : h0, nh = (ld < rd) ? h0 : h1;
+    if (fh && sp < STACK) { st.ref[sp * kBlock] = (uint32_t)fr; st.te[sp * kBlock] = fE; ++sp; }
+    if (nh && sp < STACK) { st.ref[sp * kBlock] = (uint32_t)nr; st.te[sp * kBlock] = nE; ++sp; }
+  }
+  t_out = closest;
+  ref_out = best;
+  return any;
+}
+
+// ---------------------------------------------------------------- textures
+struct Mat {
+  float4 m0, m1, m2, m3, m4;
+  __device__ __forceinline__ uint32_t flags() const { return __float_as_uint(m4.w); }
+  __device__ __forceinline__ int32_t mat_type() const { return (int32_t)(flags() & 0xfu); }
+  __device__ __forceinline__ int32_t tex_type() const { return (int32_t)((flags() >> 4) & 0xfu); }
+  __device__ __forceinline__ bool is_medium() const { return (flags() >> 8) & 1u; }
+  __device__ __forceinline__ int32_t image() const { return (int32_t)(flags() >> 16) - 1; }
+};
+
+__device__ __forceinline__ int32_t mat_index(const DevScene& sc, int32_t ref) {
+  return sc.mat_base[leaf_type(ref)] + leaf_index(ref);
+}
+__device__ __forceinline__ uint32_t mat_flags(const DevScene& sc, int32_t g) {
+  return __float_as_uint(sc.mats[5 * g + 4].w);
+}
+
+__device__ __forceinline__ float perlin_noise(const DevScene& sc, pt_v3 p) {  // kernels.py:110-151
+  float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
+  float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+  int32_t i = pt_f2i(fx), j = pt_f2i(fy), k = pt_f2i(fz);
+  float uu = u * u * (3.0f - 2.0f * u);
+  float vv = v * v * (3.0f - 2.0f * v);
+  float ww = w * w * (3.0f - 2.0f * w);
+  const int32_t* px = sc.perlin_perm;
+  const int32_t* py = sc.perlin_perm + 256;
+  const int32_t* pz = sc.perlin_perm + 512;
+  float accum = 0.0f;
+#pragma unroll
+  for (int di = 0; di < 2; ++di)
+#pragma unroll
+    for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+      for (int dk = 0; dk < 2; ++dk) {
+        int32_t idx = px[(i + di) & 255] ^ py[(j + dj) & 255] ^ pz[(k + dk) & 255];
+        float4 g = sc.perlin_vec[idx];
+        pt_v3 wt = pt_v3f(u - (float)di, v - (float)dj, w - (float)dk);
+        float fxw = di ? uu : (1.0f - uu);
+        float fyw = dj ? vv : (1.0f - vv);
+        float fzw = dk ? ww : (1.0f - ww);
+        accum += fxw * fyw * fzw * pt_dot(pt_v3f(g.x, g.y, g.z), wt);
+      }
+  return accum;
+}
+
+__device__ __forceinline__ float perlin_turb3(const DevScene& sc, pt_v3 p) {  // kernels.py:155-169
+  float accum = 0.0f, weight = 1.0f;
+  pt_v3 tp = p;
+#pragma unroll 1
+  for (int oc = 0; oc < 3; ++oc) {
+    accum += weight * perlin_noise(sc, tp);
+    weight *= 0.5f;
+    tp = pt_scale(tp, 2.0f);
+  }
+  return fabsf(accum);
+}
+
+__device__ __forceinline__ pt_v3 eval_texture(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 hp) {
+  // kernels.py:925-1017
+  int32_t tex = m.tex_type();
+  pt_v3 c1 = pt_v3f(m.m2.x, m.m2.y, m.m2.z);
+  if (tex == 0) return c1;
+  float scale = m.m2.w;
+  if (tex == 1) {
+    float inv_scale = 1.0f / scale;
+    int32_t xi = pt_f2i(floorf(inv_scale * hp.x));
+    int32_t yi = pt_f2i(floorf(inv_scale * hp.y));
+    int32_t zi = pt_f2i(floorf(inv_scale * hp.z));
+    int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
+    return (s % 2 == 0) ? c1 : pt_v3f(m.m3.x, m.m3.y, m.m3.z);
+  }
+  if (tex == 2) {
+    if (leaf_type(ref) != kSphere) return pt_v3f(1.0f, 0.0f, 1.0f);
+    int32_t img = m.image();
+    float4 s = sc.spheres[leaf_index(ref)];
+    pt_v3 n = pt_normalize(pt_sub(hp, pt_v3f(s.x, s.y, s.z)));  // get_sphere_uv, kernels.py:79-102
+    float phi = pt_acosf(-n.y);
+    float theta = pt_atan2f(-n.z, n.x) + PT_PI_F;
+    float u = theta / PT_2PI_F;
+    float v = phi / PT_PI_F;
+    if (img < 0 || img >= sc.num_images) return pt_v3f(1.0f, 1.0f, 1.0f);
+    int32_t W = sc.img_w[img], H = sc.img_h[img];
+    u = pt_maxf(0.0f, pt_minf(1.0f, u));
+    v = 1.0f - pt_maxf(0.0f, pt_minf(1.0f, v));
+    int32_t ii = pt_f2i(u * (float)W);
+    int32_t jj = pt_f2i(v * (float)H);
+    ii = ii < 0 ? 0 : (ii > W - 1 ? W - 1 : ii);
+    jj = jj < 0 ? 0 : (jj > H - 1 ? H - 1 : jj);
+    uint32_t px = sc.texels[sc.img_offset[img] + jj * W + ii];
+    return pt_v3f((float)(px & 0xffu) / 255.0f, (float)((px >> 8) & 0xffu) / 255.0f,
+                  (float)((px >> 16) & 0xffu) / 255.0f);
+  }
+  if (tex == 3) {
+    float nv = pt_sinf(scale * hp.z + 10.0f * perlin_turb3(sc, hp));
+    return pt_scale(pt_scale(c1, 0.5f), 1.0f + nv);
+  }
+  return pt_v3f(1.0f, 1.0f, 1.0f);
+}
+
+// ---------------------------------------------------------------- materials
+__device__ __forceinline__ pt_v3 reflect3(pt_v3 v, pt_v3 n) {  // kernels.py:767-769
+  return pt_sub(v, pt_scale(n, 2.0f * pt_dot(v, n)));
+}
+__device__ __forceinline__ pt_v3 refract3(pt_v3 uv, pt_v3 n, float eta) {  // kernels.py:773-778
+  float ct = pt_minf(-pt_dot(uv, n), 1.0f);
+  pt_v3 perp = pt_scale(pt_add(uv, pt_scale(n, ct)), eta);
+  pt_v3 par = pt_scale(n, -sqrtf(fabsf(1.0f - pt_dot(perp, perp))));
+  return pt_add(perp, par);
+}
+__device__ __forceinline__ float reflectance(float c, float ri) {  // kernels.py:782-786
+  float r0 = (1.0f - ri) / (1.0f + ri);
+  r0 = r0 * r0;
+  return r0 + (1.0f - r0) * pt_pow5f(1.0f - c);
+}
+
+// scatter(), kernels.py:818-917. Returns scattered; writes direction and
+// attenuation. Material record already loaded.
+__device__ __forceinline__ bool scatter(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 dir, pt_v3 hp,
+                                     pt_v3 n, Rng& r, pt_v3& sdir, pt_v3& att) {
+  int32_t mt = m.mat_type();
+  sdir = pt_v3f(0.0f, 0.0f, 0.0f);
+  att = pt_v3f(1.0f, 1.0f, 1.0f);
+  if (mt == 0) {
+    att = eval_texture(sc, ref, m, hp);
+    sdir = random_cosine_direction(n, r);
+    return true;
+  }
+  if (mt == 1) {
+    pt_v3 refl = reflect3(pt_normalize(dir), n);
+    sdir = pt_add(refl, pt_scale(random_unit_vector(r), m.m0.w));
+    if (pt_dot(sdir, n) > 0.0f) {
+      att = pt_v3f(m.m0.x, m.m0.y, m.m0.z);
+      return true;
+    }
+    return false;
+  }
+  if (mt == 2) {
+    float ir = m.m1.w;
+    bool front = pt_dot(dir, n) < 0.0f;
+    pt_v3 nf = front ? n : pt_neg(n);
+    float ratio = front ? (1.0f / ir) : ir;
+    pt_v3 ud = pt_normalize(dir);
+    float ct = pt_minf(-pt_dot(ud, nf), 1.0f);
+    float st = sqrtf(1.0f - ct * ct);
+    bool cannot = ratio * st > 1.0f;
+    float u = r.next();  // unconditional draw
+    sdir = (cannot || reflectance(ct, ratio) > u) ? reflect3(ud, nf) : refract3(ud, nf, ratio);
+    return true;
+  }
+  if (mt == 4) {
+    sdir = random_unit_vector(r);
+    att = eval_texture(sc, ref, m, hp);
+    return true;
+  }
+  return false;  // emissive (3) and unknown types
+}
+
+__device__ __forceinline__ Mat load_mat(const DevScene& sc, int32_t g) {
+  const float4* p = sc.mats + 5 * g;
+  Mat m;
+  m.m0 = p[0]; m.m1 = p[1]; m.m2 = p[2]; m.m3 = p[3]; m.m4 = p[4];
+  return m;
+}
+
+__device__ __forceinline__ pt_v3 emitted(const Mat& m) {  // kernels.py:790-814
+  return (m.mat_type() == 3) ? pt_v3f(m.m1.x, m.m1.y, m.m1.z) : pt_v3f(0.0f, 0.0f, 0.0f);
+}
+
+// Second half of apply_constant_medium (kernels.py:421-448) once the exit
+// traversal from t_entry + 1e-4 has been done. Returns is_medium_hit and the
+// scatter point; t_exit = 0 when no exit was found.
+__device__ __forceinline__ bool medium_step(bool hit_exit, float t_exit_hit, float t_entry, float density,
+                                            pt_v3 o, pt_v3 d, Rng& r, pt_v3& p, float& t_exit) {
+  t_exit = 0.0f;
+  if (!hit_exit) return false;
+  t_exit = t_exit_hit;
+  float t1 = pt_maxf(t_entry, kTMin);
+  float t2 = pt_minf(t_exit, kTMax);
+  if (t1 < t2) {
+    if (t1 < 0.0f) t1 = 0.0f;
+    float rl = sqrtf(pt_dot(d, d));
+    float inside = (t2 - t1) * rl;
+    float hd = -pt_logf(pt_maxf(r.next(), 1e-10f)) / density;
+    if (hd < inside) {
+      float ts = t1 + hd / rl;
+      p = pt_add(o, pt_scale(d, ts));
+      return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace ptmi

@@ -1,0 +1,197 @@
+// pt_megakernel.hip — depth-first integrator for gfx950.
+//
+// Replaces kernels.render_sample (kernels.py:1177-1202) + trace_ray
+// (kernels.py:1025-1170). Design (MI355X-first, not a translation):
+//   * one thread owns one pixel for a whole batch of samples and regenerates
+//     the next camera path as soon as the previous one ends, so a wave keeps
+//     all 64 lanes busy across path-length variance instead of idling until
+//     its longest path of a sample finishes;
+//   * every loop iteration runs ONE traversal for every active lane; the
+//     constant-medium exit search (kernels.py:417) is not a nested second
+//     traversal but its own iteration (mode MEDIUM_EXIT), so lanes doing it
+//     share the traversal code with lanes tracing ordinary segments;
+//   * the accumulator is read once and written once per launch (sample
+//     colours added in sample order in registers: same float sequence as
+//     accum += color per sample);
+//   * BVH: child-box BVH2 nodes (64 B, one node load tests both children),
+//     traversal stack in LDS (slot-major, conflict-free), see pt_device.hpp.
+#include "pt_device.hpp"
+
+namespace ptmi {
+
+enum : int32_t { kModeTrace = 0, kModeMediumExit = 1 };
+
+struct PathState {
+  pt_v3 o, dir, thr, color;
+  Rng rng;
+  int32_t depth;     // the reference's loop variable `depth` (kernels.py:1054)
+  int32_t mode;
+  float t_entry;     // medium boundary hit (mode MEDIUM_EXIT)
+  int32_t ref_entry;
+};
+
+__device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32_t py, int32_t s,
+                                           PathState& ps) {
+  ps.rng.key = pt_path_key(fr.seed, (uint32_t)(py * fr.width + px), (uint32_t)s);
+  ps.rng.n = 0;
+  pt_v3 d;
+  get_ray(fr, px, py, ps.rng, ps.o, d);
+  ps.dir = pt_normalize(d);  // Q1: kernels.py:1042
+  ps.thr = pt_v3f(1.0f, 1.0f, 1.0f);
+  ps.color = pt_v3f(0.0f, 0.0f, 0.0f);
+  ps.depth = 0;
+  ps.mode = kModeTrace;
+  ps.t_entry = 0.0f;
+  ps.ref_entry = 0;
+}
+
+template <int STACK>
+__global__ __launch_bounds__(kBlock) void mk_render_kernel(DevScene sc, DevFrame fr, float* __restrict__ accum,
+                                                           int32_t s_begin, int32_t s_count,
+                                                           unsigned long long* __restrict__ counters) {
+  __shared__ uint32_t lds_ref[STACK * kBlock];
+  __shared__ float lds_t[STACK * kBlock];
+  __shared__ unsigned long long blk_cnt[3];
+  const int tid = threadIdx.x;
+  if (tid < 3) blk_cnt[tid] = 0ull;
+  Stack st{lds_ref + tid, lds_t + tid};
+
+  // 16x16 pixel block = 4 waves of 8x8 (square footprints keep a wave's
+  // camera rays coherent in the BVH).
+  const int lane = tid & 63, wv = tid >> 6;
+  const int32_t lx = ((wv & 1) << 3) | (lane & 7);
+  const int32_t ly = ((wv >> 1) << 3) | (lane >> 3);
+  const int32_t px = fr.x0 + (int32_t)blockIdx.x * 16 + lx;
+  const int32_t lr = (int32_t)blockIdx.y * 16 + ly;
+  int32_t py = (lr < fr.n_rows) ? frame_row(fr, lr) : -1;
+  const bool valid = (px < fr.x0 + fr.w) && (py >= 0);
+
+  pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
+  float* ap = nullptr;
+  int32_t s = s_begin, s_end = s_begin + s_count;
+  if (valid) {
+    ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
+    acc = pt_v3f(ap[0], ap[1], ap[2]);
+  } else {
+    s = s_end;
+  }
+  unsigned long long n_seg = 0, n_med = 0, n_paths = 0;
+  const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
+  PathState ps;
+  if (s < s_end) start_path(fr, px, py, s, ps);
+  __syncthreads();
+
+  while (s < s_end) {
+    const bool exit_mode = ps.mode == kModeMediumExit;
+    const float tmin = exit_mode ? ps.t_entry + 0.0001f : kTMin;  // kernels.py:418 / 1057
+    float t;
+    int32_t ref;
+    bool hit = traverse<STACK>(sc, ps.o, ps.dir, tmin, kTMax, st, t, ref);
+    if (exit_mode) ++n_med; else ++n_seg;
+
+    bool done = false, scattered = false, passthrough = false;
+    pt_v3 hp, sdir, att;
+    if (!exit_mode) {
+      if (!hit) {
+        ps.color = pt_add(ps.color, pt_mul(ps.thr, bg));  // kernels.py:1164-1168
+        done = true;
+      } else {
+        const int32_t g = mat_index(sc, ref);
+        if ((mat_flags(sc, g) >> 8) & 1u) {  // medium boundary: exit search next iteration
+          ps.mode = kModeMediumExit;
+          ps.t_entry = t;
+          ps.ref_entry = ref;
+          continue;
+        }
+        const Mat m = load_mat(sc, g);
+        hp = pt_add(ps.o, pt_scale(ps.dir, t));
+        pt_v3 n = hit_normal(sc, ref, hp, ps.dir);
+        ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
+        scattered = scatter(sc, ref, m, ps.dir, hp, n, ps.rng, sdir, att);
+      }
+    } else {
+      ps.mode = kModeTrace;
+      const int32_t g = mat_index(sc, ps.ref_entry);
+      const Mat m = load_mat(sc, g);
+      float t_exit;
+      pt_v3 mp;
+      // apply_constant_medium, kernels.py:421-448 (density m3.w)
+      if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
+        hp = mp;  // kernels.py:1082-1097
+        sdir = random_unit_vector(ps.rng);
+        att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
+        scattered = true;
+      } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
+        passthrough = true;
+        float rl = sqrtf(pt_dot(ps.dir, ps.dir));
+        float eps_t = 0.001f / rl;
+        ps.o = pt_add(ps.o, pt_scale(ps.dir, t_exit + eps_t));
+      } else {  // fallback: shade the boundary as a surface, kernels.py:1111-1119
+        hp = pt_add(ps.o, pt_scale(ps.dir, ps.t_entry));
+        pt_v3 n = hit_normal(sc, ps.ref_entry, hp, ps.dir);
+        ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));
+        scattered = scatter(sc, ps.ref_entry, m, ps.dir, hp, n, ps.rng, sdir, att);
+      }
+    }
+
+    if (!done) {
+      if (scattered) {  // kernels.py:1131-1157
+        ps.o = hp;
+        ps.dir = sdir;
+        ps.thr = pt_mul(ps.thr, att);
+        if (ps.depth + 1 >= fr.max_depth) {
+          done = true;
+        } else {
+          if (ps.depth + 1 >= kRRMinDepth) {
+            float sp = pt_minf(pt_maxf(pt_maxf(ps.thr.x, ps.thr.y), ps.thr.z), kRRMaxProb);
+            if (ps.rng.next() > sp) done = true;
+            else ps.thr = pt_divs(ps.thr, sp);
+          }
+          if (!done) ++ps.depth;
+        }
+      } else if (passthrough) {
+        ++ps.depth;
+        if (ps.depth >= fr.max_depth) done = true;
+      } else {
+        done = true;
+      }
+    }
+    if (done) {
+      acc = pt_add(acc, ps.color);  // render_sample: accum += color (kernels.py:1187)
+      ++n_paths;
+      ++s;
+      if (s < s_end) start_path(fr, px, py, s, ps);
+    }
+  }
+  if (valid) {
+    ap[0] = acc.x;
+    ap[1] = acc.y;
+    ap[2] = acc.z;
+  }
+  if (counters) {
+    atomicAdd(&blk_cnt[0], n_seg);
+    atomicAdd(&blk_cnt[1], n_med);
+    atomicAdd(&blk_cnt[2], n_paths);
+    __syncthreads();
+    if (tid < 3) atomicAdd(counters + tid, blk_cnt[tid]);
+  }
+}
+
+template <int STACK>
+static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum, int32_t s_begin,
+                            int32_t s_count, unsigned long long* counters, hipStream_t stream) {
+  dim3 grid((unsigned)((fr.w + 15) / 16), (unsigned)((fr.n_rows + 15) / 16));
+  hipLaunchKernelGGL(mk_render_kernel<STACK>, grid, dim3(kBlock), 0, stream, sc, fr, accum, s_begin, s_count,
+                     counters);
+  return hipGetLastError();
+}
+
+hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, float* accum,
+                     int32_t s_begin, int32_t s_count, unsigned long long* counters, hipStream_t stream) {
+  if (stack_needed <= 16) return launch_mk<16>(sc, fr, accum, s_begin, s_count, counters, stream);
+  if (stack_needed <= 24) return launch_mk<24>(sc, fr, accum, s_begin, s_count, counters, stream);
+  if (stack_needed <= 32) return launch_mk<32>(sc, fr, accum, s_begin, s_count, counters, stream);
+  return launch_mk<64>(sc, fr, accum, s_begin, s_count, counters, stream);
+}
+
+}  // namespace ptmi

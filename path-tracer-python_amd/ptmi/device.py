@@ -1,0 +1,185 @@
+"""Device residency of a packed scene and thin wrappers over the C-ABI.
+
+PyTorch is used only as the device allocator / stream provider: every array
+of the packed layout (scene_data.DeviceLayout) becomes one torch tensor on
+the GPU and the C-ABI receives raw pointers (include/ptmi.h). This replaces
+the reference's module-global Taichi fields (fields.py) with a per-device
+object, so several scenes can coexist in one process.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .scene_data import DeviceLayout, SceneArrays, pack_device
+
+
+def _stream_ptr(stream=None):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise _lib.PtmiError('no GPU visible: the MI355X integrator has no CPU fallback')
+    _lib.load()
+
+
+class DeviceScene:
+    """A packed scene resident in HBM plus its ptmi_scene_view."""
+
+    def __init__(self, scene, device=None):
+        require_gpu()
+        layout = scene if isinstance(scene, DeviceLayout) else pack_device(scene)
+        self.layout = layout
+        self.device = torch.device(device if device is not None else 'cuda')
+
+        def up(a):
+            a = np.ascontiguousarray(a)
+            if a.size == 0:
+                a = np.zeros(4, dtype=a.dtype)  # keep a valid 16-B aligned pointer
+            return torch.from_numpy(a.reshape(-1).copy()).to(self.device)
+
+        self.t_nodes = up(layout.nodes)
+        self.t_spheres = up(layout.spheres)
+        self.t_quads = up(layout.quads)
+        self.t_tris = up(layout.tris)
+        self.t_mats = up(layout.mats)
+        self.t_texels = up(layout.texels.view(np.int32))
+        self.t_pvec = up(layout.perlin_vec)
+        self.t_perm = up(layout.perlin_perm)
+        v = _lib.SceneView()
+        v.nodes = self.t_nodes.data_ptr()
+        v.n_inner = layout.n_inner
+        v.root_ref = layout.root_ref
+        for k in range(3):
+            v.root_min[k] = float(layout.root_min[k])
+            v.root_max[k] = float(layout.root_max[k])
+        v.max_leaf_depth = layout.max_leaf_depth
+        v.spheres = self.t_spheres.data_ptr()
+        v.quads = self.t_quads.data_ptr()
+        v.tris = self.t_tris.data_ptr()
+        v.mats = self.t_mats.data_ptr()
+        v.num_spheres, v.num_quads, v.num_triangles = layout.num_spheres, layout.num_quads, layout.num_triangles
+        v.texels = self.t_texels.data_ptr()
+        v.num_images = len(layout.img_w)
+        for k in range(len(layout.img_w)):
+            v.img_offset[k] = layout.img_offset[k]
+            v.img_w[k] = layout.img_w[k]
+            v.img_h[k] = layout.img_h[k]
+        v.perlin_vec = self.t_pvec.data_ptr()
+        v.perlin_perm = self.t_perm.data_ptr()
+        self.view = v
+        _lib.check(_lib.load().ptmi_scene_check(C.byref(v)), 'ptmi_scene_check')
+
+    @classmethod
+    def from_arrays(cls, sa: SceneArrays, device=None):
+        return cls(pack_device(sa), device)
+
+
+def make_frame(cam, bg, max_depth, seed, width, height, window=None, band=(1, 1, 0)):
+    """ptmi_frame from camera upload values (dict of f32 3-vectors or an
+    object with the reference camera's attributes)."""
+    f = _lib.Frame()
+    get = (lambda k: cam[k]) if isinstance(cam, dict) else None
+    if get is None:
+        def vec(p):
+            return np.array([p.x, p.y, p.z], np.float64).astype(np.float32)
+        vals = {'center': vec(cam.center), 'pixel00': vec(cam.pixel00_loc), 'delta_u': vec(cam.delta_u),
+                'delta_v': vec(cam.delta_v), 'defocus_u': vec(cam.defocus_disk_u),
+                'defocus_v': vec(cam.defocus_disk_v), 'defocus_angle': float(cam.defocus_angle)}
+        get = vals.__getitem__
+    for k, fld in (('center', 'center'), ('pixel00', 'pixel00'), ('delta_u', 'delta_u'), ('delta_v', 'delta_v'),
+                   ('defocus_u', 'defocus_u'), ('defocus_v', 'defocus_v')):
+        arr = np.asarray(get(k), np.float32)
+        for i in range(3):
+            getattr(f.cam, fld)[i] = float(arr[i])
+    f.cam.defocus_angle = float(np.float32(get('defocus_angle')))
+    bgv = np.asarray([bg.x, bg.y, bg.z] if hasattr(bg, 'x') else bg, np.float64).astype(np.float32)
+    for i in range(3):
+        f.bg[i] = float(bgv[i])
+    f.max_depth = int(max_depth)
+    f.seed = int(seed) & 0xffffffff
+    f.width, f.height = int(width), int(height)
+    x0, y0, w, h = window if window is not None else (0, 0, width, height)
+    f.x0, f.y0, f.w, f.h = int(x0), int(y0), int(w), int(h)
+    f.band_rows, f.band_stride, f.band_offset = (int(b) for b in band)
+    return f
+
+
+def frame_pixel_rows(frame):
+    """Image rows owned by a frame (window + band filter), as the kernels see them."""
+    rows = [frame.y0 + r for r in range(frame.h)
+            if (r // frame.band_rows) % frame.band_stride == frame.band_offset]
+    return np.asarray(rows, np.int64)
+
+
+class Integrator:
+    """Launch wrapper: megakernel / wavefront / clear / tonemap on one stream."""
+
+    def __init__(self, dscene: DeviceScene, with_counters=True):
+        self.scene = dscene
+        self.lib = _lib.load()
+        self.counters = torch.zeros(_lib.NUM_COUNTERS, dtype=torch.int64, device=dscene.device) \
+            if with_counters else None
+        self._ws = None
+        self._ws_bytes = 0
+
+    def _cnt(self):
+        return C.c_void_p(self.counters.data_ptr()) if self.counters is not None else None
+
+    def render_mk(self, frame, accum, sample_begin, sample_count, stream=None):
+        _check_accum(accum, frame)
+        _lib.check(self.lib.ptmi_mk_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(accum.data_ptr()),
+                                           int(sample_begin), int(sample_count), self._cnt(), _stream_ptr(stream)),
+                   'ptmi_mk_render')
+
+    def workspace(self, frame):
+        need = int(self.lib.ptmi_wf_workspace_bytes(C.byref(frame)))
+        if need == 0:
+            _lib.check(-1, 'ptmi_wf_workspace_bytes')
+        if self._ws is None or self._ws_bytes < need:
+            self._ws = torch.empty((need + 15) // 16 * 4, dtype=torch.float32, device=self.scene.device)
+            self._ws_bytes = self._ws.numel() * 4
+        return self._ws
+
+    def render_wf(self, frame, accum, sample_begin, sample_count, stream=None):
+        _check_accum(accum, frame)
+        ws = self.workspace(frame)
+        _lib.check(self.lib.ptmi_wf_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(ws.data_ptr()),
+                                           self._ws_bytes, C.c_void_p(accum.data_ptr()), int(sample_begin),
+                                           int(sample_count), self._cnt(), _stream_ptr(stream)),
+                   'ptmi_wf_render')
+
+    def clear(self, frame, accum, stream=None):
+        _check_accum(accum, frame)
+        _lib.check(self.lib.ptmi_clear(C.byref(frame), C.c_void_p(accum.data_ptr()), _stream_ptr(stream)),
+                   'ptmi_clear')
+
+    def tonemap(self, accum, spp, stream=None):
+        h, w, _ = accum.shape
+        out = torch.empty((h, w, 3), dtype=torch.uint8, device=accum.device)
+        _lib.check(self.lib.ptmi_tonemap(C.c_void_p(accum.data_ptr()), C.c_void_p(out.data_ptr()), w, h, int(spp),
+                                         _stream_ptr(stream)), 'ptmi_tonemap')
+        return out
+
+    def read_counters(self):
+        if self.counters is None:
+            return None
+        c = self.counters.cpu().numpy()
+        return {'segments': int(c[0]), 'medium': int(c[1]), 'paths': int(c[2])}
+
+    def reset_counters(self):
+        if self.counters is not None:
+            self.counters.zero_()
+
+
+def _check_accum(accum, frame):
+    if not (isinstance(accum, torch.Tensor) and accum.is_cuda and accum.dtype == torch.float32
+            and accum.is_contiguous() and tuple(accum.shape) == (frame.height, frame.width, 3)):
+        raise _lib.PtmiError(f'accum must be a contiguous cuda float32 tensor of shape '
+                             f'({frame.height}, {frame.width}, 3)')

@@ -1,0 +1,307 @@
+"""Compiled-scene container in the reference's array layout, and the packer
+that turns it into the MI355X device layout of include/ptmi.h.
+
+The reference compiles a scene into per-primitive-type numpy arrays
+(src/render_server/taichi_renderer/scene_compiler.py:931-965) and a flattened
+SAH BVH (bvh_compiler.py:132-168, sah_bvh_builder.py:338-418) and then
+uploads them field by field (renderer.py:102-228). ``SceneArrays`` keeps
+exactly those arrays (same names, dtypes and shapes) so fixtures captured from
+the reference compare array-for-array; ``pack_device`` produces the packed
+GPU layout (child-box BVH2 nodes, 16-float quads, 20-float materials, RGBA8
+texels) documented in include/ptmi.h.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+PRIM_SPHERE, PRIM_TRIANGLE, PRIM_QUAD = 0, 1, 2  # scene_compiler.py:10-12
+MAX_IMAGES = 16
+
+# per-type material array names (compile_materials, scene_compiler.py:425-439)
+MAT_KEYS = ('material_type', 'material_albedo', 'material_fuzz', 'material_ir', 'material_emit_color',
+            'texture_type', 'texture_scale', 'texture_color1', 'texture_color2', 'texture_image_idx',
+            'is_constant_medium', 'medium_density', 'medium_albedo')
+BVH_KEYS = ('bvh_bbox_min', 'bvh_bbox_max', 'bvh_left_child', 'bvh_right_child', 'bvh_parent',
+            'bvh_prim_type', 'bvh_prim_idx')
+QUAD_KEYS = ('quad_Q', 'quad_u', 'quad_v', 'quad_normal', 'quad_D', 'quad_w')
+TRI_KEYS = ('triangle_v0', 'triangle_v1', 'triangle_v2', 'triangle_edge1', 'triangle_edge2', 'triangle_normal')
+PERLIN_KEYS = ('perlin_randvec', 'perlin_perm_x', 'perlin_perm_y', 'perlin_perm_z')
+
+_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..', 'tests', 'golden')
+
+
+def _empty_mats(n):
+    return {
+        'material_type': np.zeros(n, np.int32), 'material_albedo': np.zeros((n, 3), np.float32),
+        'material_fuzz': np.zeros(n, np.float32), 'material_ir': np.zeros(n, np.float32),
+        'material_emit_color': np.zeros((n, 3), np.float32), 'texture_type': np.zeros(n, np.int32),
+        'texture_scale': np.ones(n, np.float32), 'texture_color1': np.zeros((n, 3), np.float32),
+        'texture_color2': np.zeros((n, 3), np.float32), 'texture_image_idx': np.full(n, -1, np.int32),
+        'is_constant_medium': np.zeros(n, np.int32), 'medium_density': np.zeros(n, np.float32),
+        'medium_albedo': np.zeros((n, 3), np.float32),
+    }
+
+
+@dataclass
+class SceneArrays:
+    """Reference-layout compiled scene (geometry, materials, BVH, Perlin, images)."""
+    sphere_data: np.ndarray
+    sphere_mats: dict
+    quads: dict
+    quad_mats: dict
+    tris: dict
+    tri_mats: dict
+    bvh: dict
+    perlin: dict
+    images: list = field(default_factory=list)  # (H, W, 3) uint8 each
+
+    @property
+    def num_spheres(self):
+        return int(self.sphere_data.shape[0])
+
+    @property
+    def num_quads(self):
+        return int(self.quads['quad_Q'].shape[0])
+
+    @property
+    def num_triangles(self):
+        return int(self.tris['triangle_v0'].shape[0])
+
+    @property
+    def num_bvh_nodes(self):
+        return int(self.bvh['bvh_bbox_min'].shape[0])
+
+    def mats(self, prim_type):
+        return {PRIM_SPHERE: self.sphere_mats, PRIM_TRIANGLE: self.tri_mats, PRIM_QUAD: self.quad_mats}[prim_type]
+
+    # ------------------------------------------------------------ constructors
+    @classmethod
+    def from_compiled(cls, geometry, materials, quad_geometry, quad_materials, tri_geometry, tri_materials,
+                      bvh, perlin, images):
+        """From compile_scene()/compile_bvh() outputs (reference or ptmi)."""
+        ns = int(geometry['num_spheres'])
+        nq = int(quad_geometry['num_quads'])
+        nt = int(tri_geometry['num_triangles'])
+        sd = np.asarray(geometry['sphere_data'], np.float32).reshape(ns, 4)
+        q = {k: np.asarray(quad_geometry[k], np.float32).reshape((nq,) if k == 'quad_D' else (nq, 3))
+             for k in QUAD_KEYS}
+        t = {k: np.asarray(tri_geometry[k], np.float32).reshape(nt, 3) for k in TRI_KEYS}
+
+        def fix(m, n):
+            out = _empty_mats(n)
+            for k in MAT_KEYS:
+                if k in m:
+                    out[k] = np.asarray(m[k], out[k].dtype).reshape(out[k].shape)
+            return out
+
+        b = {k: np.asarray(bvh[k], np.float32 if 'bbox' in k else np.int32) for k in BVH_KEYS}
+        b['bvh_bbox_min'] = b['bvh_bbox_min'].reshape(-1, 3)
+        b['bvh_bbox_max'] = b['bvh_bbox_max'].reshape(-1, 3)
+        p = {'perlin_randvec': np.asarray(perlin['perlin_randvec'], np.float32).reshape(256, 3)}
+        for k in PERLIN_KEYS[1:]:
+            p[k] = np.asarray(perlin[k], np.int32).reshape(256)
+        return cls(sd, fix(materials, ns), q, fix(quad_materials, nq), t, fix(tri_materials, nt), b, p,
+                   [np.ascontiguousarray(im, dtype=np.uint8) for im in images])
+
+    @classmethod
+    def from_npz(cls, path, images=None):
+        """Load a tests/golden/<scene>.npz fixture (see gen_fixtures.py)."""
+        z = np.load(path)
+        geom = {'sphere_data': z['sph_sphere_data'], 'num_spheres': z['sph_sphere_data'].shape[0]}
+        mats = {k: z['sphm_' + k] for k in MAT_KEYS}
+        qg = {k: z[k] for k in QUAD_KEYS}
+        qg['num_quads'] = z['quad_Q'].shape[0]
+        qm = {k: z['quadm_' + k] for k in MAT_KEYS}
+        tg = {k: z[k] for k in TRI_KEYS}
+        tg['num_triangles'] = z['triangle_v0'].shape[0]
+        tm = {k: z['trim_' + k] for k in MAT_KEYS}
+        bvh = {k: z[k] for k in BVH_KEYS}
+        per = {k: z[k] for k in PERLIN_KEYS}
+        if images is None:
+            used = max(int(np.max(z['sphm_texture_image_idx'], initial=-1)),
+                       int(np.max(z['quadm_texture_image_idx'], initial=-1)),
+                       int(np.max(z['trim_texture_image_idx'], initial=-1)))
+            images = [load_earthmap()] if used >= 0 else []
+        return cls.from_compiled(geom, mats, qg, qm, tg, tm, bvh, per, images)
+
+
+def golden_dir():
+    return os.path.normpath(_GOLDEN)
+
+
+def load_earthmap():
+    """Decoded RGB8 earthmap (the only image texture the BASELINE scenes use)."""
+    return np.load(os.path.join(golden_dir(), 'earthmap_u8.npz'))['earthmap']
+
+
+def load_fixture(name):
+    return SceneArrays.from_npz(os.path.join(golden_dir(), name + '.npz'))
+
+
+def fixture_camera(name, width):
+    """f32 camera upload values captured from the reference (renderer.py:230-247)."""
+    z = np.load(os.path.join(golden_dir(), name + '.npz'))
+    tag = f'cam{width}_'
+    cam = {k: np.asarray(z[tag + k], np.float32) for k in
+           ('center', 'pixel00', 'delta_u', 'delta_v', 'defocus_u', 'defocus_v')}
+    cam['defocus_angle'] = float(z[tag + 'defocus_angle'])
+    cam['width'], cam['height'] = (int(v) for v in z[tag + 'size'])
+    return cam
+
+
+def fixture_manifest():
+    with open(os.path.join(golden_dir(), 'manifest.json')) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- packing
+LEAF_FLAG = np.int64(0x80000000)
+
+
+def leaf_code(prim_type, prim_idx):
+    code = LEAF_FLAG | (np.int64(prim_type) << 28) | np.int64(prim_idx)
+    return np.int32(np.int64(code) - (1 << 32))  # as signed int32 bits
+
+
+@dataclass
+class DeviceLayout:
+    """Host-side arrays in the device layout of include/ptmi.h."""
+    nodes: np.ndarray       # (n_inner, 16) f32
+    root_ref: int
+    root_min: np.ndarray
+    root_max: np.ndarray
+    max_leaf_depth: int
+    spheres: np.ndarray     # (ns, 4) f32
+    quads: np.ndarray       # (nq, 16) f32
+    tris: np.ndarray        # (nt, 12) f32
+    mats: np.ndarray        # (ns+nq+nt, 20) f32
+    texels: np.ndarray      # (sum H*W,) u32 RGBA8
+    img_offset: list
+    img_w: list
+    img_h: list
+    perlin_vec: np.ndarray  # (256, 4) f32
+    perlin_perm: np.ndarray  # (768,) i32
+    num_spheres: int
+    num_quads: int
+    num_triangles: int
+
+    @property
+    def n_inner(self):
+        return int(self.nodes.shape[0])
+
+    def nbytes(self):
+        return sum(int(a.nbytes) for a in (self.nodes, self.spheres, self.quads, self.tris, self.mats,
+                                              self.texels, self.perlin_vec, self.perlin_perm))
+
+
+def _pack_mats(m, n):
+    out = np.zeros((n, 20), np.float32)
+    out[:, 0:3] = m['material_albedo']
+    out[:, 3] = m['material_fuzz']
+    out[:, 4:7] = m['material_emit_color']
+    out[:, 7] = m['material_ir']
+    out[:, 8:11] = m['texture_color1']
+    out[:, 11] = m['texture_scale']
+    out[:, 12:15] = m['texture_color2']
+    out[:, 15] = m['medium_density']
+    out[:, 16:19] = m['medium_albedo']
+    mt = m['material_type'].astype(np.int64)
+    tt = m['texture_type'].astype(np.int64)
+    if n and (mt.min() < 0 or mt.max() > 15 or tt.min() < 0 or tt.max() > 15):
+        raise ValueError('material/texture type codes must be in [0, 15]')
+    med = (m['is_constant_medium'] > 0).astype(np.int64)
+    img = m['texture_image_idx'].astype(np.int64) + 1
+    if n and (img.min() < 0 or img.max() > 0xffff):
+        raise ValueError('texture image index out of range')
+    flags = (mt | (tt << 4) | (med << 8) | (img << 16)).astype(np.uint32)
+    out[:, 19] = flags.view(np.float32)
+    return out
+
+
+def leaf_depths(bvh):
+    """Depth of every node (root = 0) of a preorder flattened BVH."""
+    left, right = bvh['bvh_left_child'], bvh['bvh_right_child']
+    n = left.shape[0]
+    depth = np.zeros(n, np.int32)
+    for i in range(n):  # preorder: parents precede children
+        if left[i] >= 0:
+            depth[left[i]] = depth[i] + 1
+        if right[i] >= 0:
+            depth[right[i]] = depth[i] + 1
+    return depth
+
+
+def pack_device(sa: SceneArrays) -> DeviceLayout:
+    ns, nq, nt = sa.num_spheres, sa.num_quads, sa.num_triangles
+    b = sa.bvh
+    bmin, bmax = b['bvh_bbox_min'], b['bvh_bbox_max']
+    left, right = b['bvh_left_child'], b['bvh_right_child']
+    ptype, pidx = b['bvh_prim_type'], b['bvh_prim_idx']
+    n = bmin.shape[0]
+    if n != (2 * (ns + nq + nt) - 1 if (ns + nq + nt) else 0):
+        raise ValueError(f'BVH has {n} nodes for {ns + nq + nt} primitives (expected 2N-1)')
+    is_leaf = pidx >= 0
+    internal = np.nonzero(~is_leaf)[0]
+    if np.any(left[internal] < 0) or np.any(right[internal] < 0):
+        raise ValueError('internal BVH node with a missing child')
+    cidx = np.full(n, -1, np.int64)
+    cidx[internal] = np.arange(internal.shape[0])
+    codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | pidx.astype(np.int64)) - (1 << 32)).astype(np.int32)
+    refs = np.where(is_leaf, codes, cidx.astype(np.int32)).astype(np.int32)
+    nodes = np.zeros((internal.shape[0], 16), np.float32)
+    if internal.size:
+        l, r = left[internal], right[internal]
+        nodes[:, 0:3] = bmin[l]
+        nodes[:, 3:6] = bmax[l]
+        nodes[:, 6:9] = bmin[r]
+        nodes[:, 9:12] = bmax[r]
+        nodes[:, 12] = refs[l].view(np.float32)
+        nodes[:, 13] = refs[r].view(np.float32)
+    if n:
+        root_ref = int(refs[0])
+        root_min, root_max = bmin[0].copy(), bmax[0].copy()
+        max_leaf_depth = int(leaf_depths(b).max())
+    else:
+        root_ref, root_min, root_max, max_leaf_depth = 0, np.zeros(3, np.float32), np.zeros(3, np.float32), 0
+    spheres = np.ascontiguousarray(sa.sphere_data, np.float32).reshape(ns, 4)
+    q = sa.quads
+    quads = np.zeros((nq, 16), np.float32)
+    quads[:, 0:3] = q['quad_normal']
+    quads[:, 3] = q['quad_D']
+    quads[:, 4:7] = q['quad_Q']
+    quads[:, 7:10] = q['quad_u']
+    quads[:, 10:13] = q['quad_v']
+    quads[:, 13:16] = q['quad_w']
+    t = sa.tris
+    tris = np.zeros((nt, 12), np.float32)
+    tris[:, 0:3] = t['triangle_v0']
+    tris[:, 3:6] = t['triangle_edge1']
+    tris[:, 6:9] = t['triangle_edge2']
+    tris[:, 9:12] = t['triangle_normal']
+    mats = np.concatenate([_pack_mats(sa.sphere_mats, ns), _pack_mats(sa.quad_mats, nq),
+                           _pack_mats(sa.tri_mats, nt)], axis=0)
+    if len(sa.images) > MAX_IMAGES:
+        raise ValueError(f'at most {MAX_IMAGES} image textures')
+    texels, offs, ws, hs, off = [], [], [], [], 0
+    for im in sa.images:
+        h, w, _ = im.shape
+        rgba = np.zeros((h, w, 4), np.uint8)
+        rgba[..., :3] = im
+        texels.append(rgba.reshape(-1).view(np.uint32))
+        offs.append(off)
+        ws.append(w)
+        hs.append(h)
+        off += h * w
+    texels = np.concatenate(texels) if texels else np.zeros(1, np.uint32)
+    pv = np.zeros((256, 4), np.float32)
+    pv[:, :3] = sa.perlin['perlin_randvec']
+    perm = np.concatenate([sa.perlin['perlin_perm_x'], sa.perlin['perlin_perm_y'],
+                           sa.perlin['perlin_perm_z']]).astype(np.int32)
+    if perm.min() < 0 or perm.max() > 255:
+        raise ValueError('Perlin permutation out of range')
+    return DeviceLayout(nodes, root_ref, root_min, root_max, max_leaf_depth, spheres, quads, tris, mats,
+                        texels, offs, ws, hs, pv, perm, ns, nq, nt)
