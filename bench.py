@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""bench.py — MI355X path-tracing integrator benchmark (driver contract).
+
+Metric (BASELINE.json): Msamples/s (+ achieved HBM GB/s) on vol2_final_scene
+800x800 at 1/2/4/8 MI355X. One sample = one camera path for one pixel
+(renderer.py:453-471 prints the same quantity as "M pix/s" at 1 spp/launch).
+
+Workload (BASELINE.json configs[2], the north-star target): vol2_final_scene
+800x800, wavefront integrator, 1024 spp per GPU = --steps 16 x
+--spp-per-step 64 by default. A "step" is one call of the hot path over the
+whole image for spp-per-step samples. Scene = the reference's own
+vol2_final_scene compiled arrays captured at random.seed(1234)
+(tests/golden/vol2_final_scene.npz), camera from the reference's camera math.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
+per GPU; rank r renders its own disjoint shard of sample indices of the full
+image (weak scaling: per-GPU work fixed), then one RCCL reduce (sum) of the
+f32 accumulators to rank 0 inside the timed region. value = samples of all
+ranks / max-over-ranks wall time.
+
+Rank 0 at N=1 also times the CPU oracle (oracle/, a C restatement of the
+reference's kernels.py: the reference's ti.cpu path cannot run here, Taichi is
+absent) on a bounded slice of the same workload, and reports the dominant
+kernel's roofline from HIP events recorded around its launches in the timed
+region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'path-tracer-python_amd'))
+
+METRIC = 'Msamples/s + achieved HBM GB/s, vol2_final_scene 800x800 at 1/2/4/8 MI355X'
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+BG = {'vol2_final_scene': (0.0, 0.0, 0.0), 'wavefront_comparison': (0.7, 0.8, 1.0), 'cornell_smoke': (0.0, 0.0, 0.0)}
+
+# Algorithmic HBM bytes per unit (DESIGN.md "Roofline"): what each kernel must
+# move at minimum for one unit of work in the queue layout of pt_wavefront.hip.
+ALGO_BYTES = {
+    # read o,d (24 B) + write hit t,ref (8 B) per ray
+    'wf_intersect': ('rays', 32),
+    # read ray record 48 B + hit 8 B, write next record 48 B
+    'wf_shade': ('rays', 104),
+    # read medium index 4 B + hit 8 B + ray 48 B, write next record 48 B
+    'wf_medium': ('medium rays', 108),
+    # accumulator read + write, 24 B per pixel per launch
+    'megakernel': ('pixel-launches', 24),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
+    p.add_argument('--steps', type=int, default=16)
+    p.add_argument('--warmup', type=int, default=2)
+    p.add_argument('--spp-per-step', type=int, default=64)
+    p.add_argument('--variant', choices=('wf', 'mk'), default='wf')
+    p.add_argument('--scene', default='vol2_final_scene')
+    p.add_argument('--width', type=int, default=800)
+    p.add_argument('--max-depth', type=int, default=50)
+    p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--cpu-seconds', type=float, default=12.0)
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--save-image', default='')
+    return p.parse_args()
+
+
+def cpu_baseline(scene, width, variant, max_depth, seed, budget_s):
+    """Time the CPU oracle on a bounded slice of the workload (rank 0, N=1)."""
+    import numpy as np
+    import oracle
+    from ptmi import scene_data as sd
+    sa = sd.load_fixture(scene)
+    cam = sd.fixture_camera(scene, width)
+    W, H = cam['width'], cam['height']
+    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+    osc = oracle.OracleScene(sa)
+    fr = oracle.make_frame(cam, BG[scene], max_depth, seed, W, H)
+    acc = np.zeros((H, W, 3), np.float32)
+    rows = min(H, 64)
+    y0 = (H - rows) // 2
+    t = time.perf_counter()
+    oracle.render(osc, fr, variant, acc, (0, y0, W, rows), 0, 1, threads)
+    t1 = time.perf_counter() - t
+    spp = max(1, int(budget_s / max(t1, 1e-3)))
+    t = time.perf_counter()
+    oracle.render(osc, fr, variant, acc, (0, y0, W, rows), 1, spp, threads)
+    dt = time.perf_counter() - t
+    n = W * rows * spp
+    return {'value': round(n / dt / 1e6, 4), 'unit': 'Msamples/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{scene} {W}x{H}, rows {y0}..{y0 + rows - 1} ({W}x{rows} px) x {spp} spp, '
+                      f'{"wavefront" if variant == "wf" else "megakernel"} semantics, C oracle '
+                      f'(restatement of kernels.py; Taichi ti.cpu absent), {dt:.1f} s'}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from ptmi import device, scene_data as sd, _lib
+
+    world = a.gpus
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    dev = torch.device('cuda', local_rank)
+
+    sa = sd.load_fixture(a.scene)
+    cam = sd.fixture_camera(a.scene, a.width)
+    W, H = cam['width'], cam['height']
+    integ = device.Integrator(device.DeviceScene(sd.pack_device(sa), dev))
+    frame = device.make_frame(cam, BG[a.scene], a.max_depth, a.seed, W, H)
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+    render = integ.render_mk if a.variant == 'mk' else integ.render_wf
+    sps = a.spp_per_step
+
+    def sample_base(step):  # disjoint sample shards per rank and step
+        return (step * world + rank) * sps
+
+    for k in range(a.warmup):
+        render(frame, acc, sample_base(k), sps)
+    torch.cuda.synchronize(dev)
+    integ.clear(frame, acc)
+    integ.reset_counters()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+
+    with _lib.KernelTimer(max_launches=100_000) as kt:
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(a.steps):
+            render(frame, acc, sample_base(a.warmup + k), sps)
+        if world > 1:
+            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    cnt = integ.read_counters()
+    samples_rank = W * H * sps * a.steps
+    samples_all = samples_rank * world
+    value = samples_all / elapsed / 1e6
+
+    prof = kt.result
+    dom = max((k for k in prof if prof[k]['launches']), key=lambda k: prof[k]['ms'])
+    unit_name, unit_bytes = ALGO_BYTES[dom]
+    units = {'wf_intersect': cnt['segments'], 'wf_shade': cnt['segments'], 'wf_medium': cnt['medium'],
+             'megakernel': W * H * prof['megakernel']['launches']}[dom]
+    dom_ms = prof[dom]['ms']
+    launches = prof[dom]['launches']
+    achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    S = cnt['segments'] / samples_rank
+    M = cnt['medium'] / samples_rank
+    b_sample = 44 + 24 + 128 * S  # SURVEY.md §8d whole-pipeline algorithmic bytes per sample
+
+    out = {
+        'metric': METRIC,
+        'value': round(value, 3),
+        'unit': 'Msamples/s',
+        'n_gpus': world,
+        'steps': a.steps,
+        'warmup': a.warmup,
+        'ms_per_step': round(elapsed * 1e3 / a.steps, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'reference scene vol2_final_scene compiled at random.seed(1234) (tests/golden fixture); '
+                'no external dataset',
+        'config': {
+            'workload': f'{a.scene} {W}x{H}, {"wavefront" if a.variant == "wf" else "megakernel"} integrator, '
+                        f'{sps * a.steps} spp per GPU ({a.steps} steps x {sps} spp), max_depth {a.max_depth}',
+            'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'spp_per_step': sps,
+            'spp_per_gpu': sps * a.steps, 'max_depth': a.max_depth, 'seed': a.seed,
+            'parallelism': f'sample-shard x{world} + RCCL reduce' if world > 1 else 'single GPU',
+        },
+        'roofline': {
+            'bound': 'hbm', 'kernel': dom,
+            'achieved': round(achieved, 3), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+            'frac': round(achieved / HBM_PEAK_GBPS, 6), 'traffic': None,
+            'algorithmic_bytes_per_launch': round(units * unit_bytes / max(1, launches), 1),
+            'unit_of_work': f'{unit_bytes} B per {unit_name[:-1] if unit_name.endswith("s") else unit_name}',
+            'avg_launch_ms': round(dom_ms / max(1, launches), 5),
+            'launches': launches,
+            'timing_truncated': bool(kt.truncated),
+        },
+        'kernels_ms': {k: round(v['ms'], 3) for k, v in prof.items() if v['launches']},
+        'segments_per_sample': round(S, 4),
+        'medium_traversals_per_sample': round(M, 4),
+        'pipeline_algorithmic_GBps': round(value * 1e6 * b_sample / 1e9, 3),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(a.scene, a.width, a.variant, a.max_depth, a.seed, a.cpu_seconds)
+    elif rank == 0:
+        out['cpu_baseline'] = None
+    if rank == 0:
+        if a.save_image:
+            from PIL import Image
+            img = integ.tonemap(acc, sps * a.steps * world).cpu().numpy()
+            Image.fromarray(img).save(a.save_image)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -143,6 +143,17 @@ int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int
                        int32_t *left, int32_t *right, int32_t *parent, int32_t *prim_type,
                        int32_t *prim_idx, int32_t *n_nodes);
 
+/* Per-kernel device timing of this library's own launches (HIP events on
+ * the launch stream; the reference's Taichi kernel profiler, renderer.py:15-16).
+ * ptmi_prof_start pre-creates events for max_launches launches; render calls
+ * then record around every kernel; ptmi_prof_stop synchronises, returns the
+ * summed milliseconds and launch counts per kernel kind
+ * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 wf_shade, 4 wf_medium}
+ * and disables timing. Not thread-safe; one profiling session per process. */
+#define PTMI_PROF_KINDS 5
+int ptmi_prof_start(int32_t max_launches);
+int ptmi_prof_stop(double *ms_by_kernel, uint64_t *launches_by_kernel, int32_t n_kinds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "pt_device.hpp"
+#include "pt_prof.hpp"
 
 namespace ptmi {
 hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, float* accum,
@@ -231,6 +232,24 @@ int ptmi_tonemap(const float* accum, uint8_t* out, int32_t width, int32_t height
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(tonemap_kernel, dim3(g), dim3(kBlock), 0, (hipStream_t)stream, accum, out, (int32_t)n, scale);
   return check_hip(hipGetLastError(), "tonemap launch");
+}
+
+int ptmi_prof_start(int32_t max_launches) {
+  if (max_launches < 0) return fail(PTMI_EINVAL, "max_launches < 0");
+  if (prof_start(max_launches)) return fail(PTMI_EHIP, "hipEventCreate failed");
+  return PTMI_OK;
+}
+
+int ptmi_prof_stop(double* ms_by_kernel, uint64_t* launches_by_kernel, int32_t n_kinds) {
+  if (!ms_by_kernel || !launches_by_kernel || n_kinds < 0) return fail(PTMI_EINVAL, "bad arguments");
+  int rc = prof_stop(ms_by_kernel, launches_by_kernel, n_kinds < kProfKinds ? n_kinds : kProfKinds);
+  for (int32_t k = kProfKinds; k < n_kinds; ++k) {
+    ms_by_kernel[k] = 0.0;
+    launches_by_kernel[k] = 0;
+  }
+  if (rc < 0) return fail(PTMI_EHIP, "event timing failed");
+  if (rc > 0) return fail(PTMI_ECAPACITY, "more launches than the profiling pool; counts truncated");
+  return PTMI_OK;
 }
 
 }  // extern "C"

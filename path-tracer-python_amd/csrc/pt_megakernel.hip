@@ -16,6 +16,7 @@
 //   * BVH: child-box BVH2 nodes (64 B, one node load tests both children),
 //     traversal stack in LDS (slot-major, conflict-free), see pt_device.hpp.
 #include "pt_device.hpp"
+#include "pt_prof.hpp"
 
 namespace ptmi {
 
@@ -181,8 +182,10 @@ template <int STACK>
 static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum, int32_t s_begin,
                             int32_t s_count, unsigned long long* counters, hipStream_t stream) {
   dim3 grid((unsigned)((fr.w + 15) / 16), (unsigned)((fr.n_rows + 15) / 16));
+  prof_begin(kProfMk, stream);
   hipLaunchKernelGGL(mk_render_kernel<STACK>, grid, dim3(kBlock), 0, stream, sc, fr, accum, s_begin, s_count,
                      counters);
+  prof_end(kProfMk, stream);
   return hipGetLastError();
 }
 

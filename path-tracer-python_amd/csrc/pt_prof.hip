@@ -1,0 +1,73 @@
+// pt_prof.hip — optional per-kernel HIP-event timing of the integrator's own
+// launches (the reference's equivalent is Taichi's kernel profiler,
+// renderer.py:15-16 / interactive_viewer.py:241-247). Events are recorded on
+// the launch stream right before and after each kernel, so elapsed times are
+// the kernels' device durations; collection synchronises once at the end.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "pt_prof.hpp"
+
+namespace ptmi {
+namespace {
+struct Prof {
+  bool on = false;
+  std::vector<hipEvent_t> ev;   // pairs
+  std::vector<int32_t> kind;    // one per pair
+  size_t used = 0;              // events used
+  bool overflow = false;
+};
+Prof g_prof;
+}  // namespace
+
+void prof_begin(int32_t kind, hipStream_t s) {
+  if (!g_prof.on) return;
+  if (g_prof.used + 2 > g_prof.ev.size()) {
+    g_prof.overflow = true;
+    return;
+  }
+  g_prof.kind.push_back(kind);
+  (void)hipEventRecord(g_prof.ev[g_prof.used], s);
+}
+
+void prof_end(int32_t kind, hipStream_t s) {
+  (void)kind;
+  if (!g_prof.on || g_prof.used + 2 > g_prof.ev.size()) return;
+  (void)hipEventRecord(g_prof.ev[g_prof.used + 1], s);
+  g_prof.used += 2;
+}
+
+int prof_start(int32_t max_launches) {
+  for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
+  g_prof = Prof();
+  if (max_launches <= 0) return 0;
+  g_prof.ev.resize(2 * (size_t)max_launches);
+  for (auto& e : g_prof.ev)
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+  g_prof.kind.reserve((size_t)max_launches);
+  g_prof.on = true;
+  return 0;
+}
+
+int prof_stop(double* ms, uint64_t* launches, int32_t n_kinds) {
+  for (int32_t k = 0; k < n_kinds; ++k) {
+    ms[k] = 0.0;
+    launches[k] = 0;
+  }
+  int rc = g_prof.overflow ? 1 : 0;
+  if (g_prof.used >= 2 && hipEventSynchronize(g_prof.ev[g_prof.used - 1]) != hipSuccess) rc = -1;
+  for (size_t p = 0; p + 1 < g_prof.used; p += 2) {
+    float t = 0.0f;
+    if (hipEventElapsedTime(&t, g_prof.ev[p], g_prof.ev[p + 1]) != hipSuccess) { rc = -1; continue; }
+    int32_t k = g_prof.kind[p / 2];
+    if (k >= 0 && k < n_kinds) {
+      ms[k] += (double)t;
+      launches[k] += 1;
+    }
+  }
+  for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
+  g_prof = Prof();
+  return rc;
+}
+}  // namespace ptmi

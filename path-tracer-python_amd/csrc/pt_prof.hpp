@@ -1,0 +1,13 @@
+// pt_prof.hpp — per-kernel event timing hooks (see pt_prof.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptmi {
+enum : int32_t { kProfMk = 0, kProfWfGenerate = 1, kProfWfIntersect = 2, kProfWfShade = 3, kProfWfMedium = 4,
+                 kProfKinds = 5 };
+void prof_begin(int32_t kind, hipStream_t s);
+void prof_end(int32_t kind, hipStream_t s);
+int prof_start(int32_t max_launches);
+int prof_stop(double* ms, uint64_t* launches, int32_t n_kinds);
+}  // namespace ptmi

@@ -45,7 +45,9 @@ class Frame(C.Structure):
 
 
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_wf_workspace_bytes',
-           'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah')
+           'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
+           'ptmi_prof_stop')
+PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium')
 
 _lib = None
 
@@ -76,6 +78,8 @@ def load(path: str = LIB_PATH):
     lib.ptmi_tonemap.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P]
     lib.ptmi_bvh_build_sah.argtypes = [P, C.c_int32, P, C.c_int32, P, C.c_int32, P, P, P, P, P, P, P,
                                        C.POINTER(C.c_int32)]
+    lib.ptmi_prof_start.argtypes = [C.c_int32]
+    lib.ptmi_prof_stop.argtypes = [P, P, C.c_int32]
     if lib.ptmi_version() != 1:
         raise PtmiError('libptmi ABI version mismatch')
     _lib = lib
@@ -87,3 +91,26 @@ def check(rc: int, what: str):
         msg = load().ptmi_last_error().decode(errors='replace')
         raise PtmiError(f'{what} failed ({rc}): {msg}')
     return rc
+
+
+class KernelTimer:
+    """Per-kernel device time of libptmi's own launches (ptmi_prof_start/stop)."""
+
+    def __init__(self, max_launches=200000):
+        self.max_launches = int(max_launches)
+
+    def __enter__(self):
+        check(load().ptmi_prof_start(self.max_launches), 'ptmi_prof_start')
+        self.result = None
+        return self
+
+    def __exit__(self, *exc):
+        import numpy as np
+        ms = np.zeros(len(PROF_KINDS), np.float64)
+        n = np.zeros(len(PROF_KINDS), np.uint64)
+        rc = load().ptmi_prof_stop(C.c_void_p(ms.ctypes.data), C.c_void_p(n.ctypes.data), len(PROF_KINDS))
+        self.truncated = rc == PTMI_ECAPACITY  # more launches than events: totals cover the first ones
+        if not self.truncated:
+            check(rc, 'ptmi_prof_stop')
+        self.result = {k: {'ms': float(ms[i]), 'launches': int(n[i])} for i, k in enumerate(PROF_KINDS)}
+        return False

@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU-box driver: each GPU step under its own timeout; stop on crash/timeout
+# (exit codes other than 0/1), continue past plain test failures.
+set -u
+mkdir -p gpurun_out
+step() {
+  local name=$1; shift
+  local t=$1; shift
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -n 25 "gpurun_out/$name.log"
+  echo "=== $name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    parity) step parity 900 python -m pytest tests -m gpu -x -q -s ;;
+    explore) step explore 600 python tools/gpu_explore.py ;;
+    bench) step bench 600 python bench.py ;;
+    benchmk) step benchmk 600 python bench.py --variant mk --no-cpu-baseline ;;
+    rocprof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 4 --no-cpu-baseline ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
