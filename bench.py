@@ -67,6 +67,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--save-image', default='')
+    p.add_argument('--shard', choices=('samples', 'tiles'), default='samples',
+                   help='multi-GPU partition: disjoint sample shards (weak scaling) or row-band tiles (strong)')
     return p.parse_args()
 
 
@@ -103,6 +105,7 @@ def main():
     import torch
     import torch.distributed as dist
     from ptmi import device, scene_data as sd, _lib
+    from ptmi.distributed import Shard, max_over_ranks, reduce_accum
 
     world = a.gpus
     rank = int(os.environ.get('RANK', '0'))
@@ -117,13 +120,14 @@ def main():
     cam = sd.fixture_camera(a.scene, a.width)
     W, H = cam['width'], cam['height']
     integ = device.Integrator(device.DeviceScene(sd.pack_device(sa), dev))
-    frame = device.make_frame(cam, BG[a.scene], a.max_depth, a.seed, W, H)
+    shard = Shard(rank, world, a.shard)
+    frame = device.make_frame(cam, BG[a.scene], a.max_depth, a.seed, W, H, band=shard.band())
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     render = integ.render_mk if a.variant == 'mk' else integ.render_wf
     sps = a.spp_per_step
 
-    def sample_base(step):  # disjoint sample shards per rank and step
-        return (step * world + rank) * sps
+    def sample_base(step):
+        return shard.sample_range(step, sps)[0]
 
     for k in range(a.warmup):
         render(frame, acc, sample_base(k), sps)
@@ -141,26 +145,23 @@ def main():
         t0 = time.perf_counter()
         for k in range(a.steps):
             render(frame, acc, sample_base(a.warmup + k), sps)
-        if world > 1:
-            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        reduce_accum(acc, dst=0)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
     cnt = integ.read_counters()
-    samples_rank = W * H * sps * a.steps
-    samples_all = samples_rank * world
+    rows_rank = len(shard.rows(H))
+    samples_rank = W * rows_rank * sps * a.steps
+    samples_all = samples_rank * world if a.shard == 'samples' else W * H * sps * a.steps
     value = samples_all / elapsed / 1e6
 
     prof = kt.result
     dom = max((k for k in prof if prof[k]['launches']), key=lambda k: prof[k]['ms'])
     unit_name, unit_bytes = ALGO_BYTES[dom]
     units = {'wf_intersect': cnt['segments'], 'wf_shade': cnt['segments'], 'wf_medium': cnt['medium'],
-             'megakernel': W * H * prof['megakernel']['launches']}[dom]
+             'megakernel': W * rows_rank * prof['megakernel']['launches']}[dom]
     dom_ms = prof[dom]['ms']
     launches = prof[dom]['launches']
     achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -177,7 +178,7 @@ def main():
         'warmup': a.warmup,
         'ms_per_step': round(elapsed * 1e3 / a.steps, 4),
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': 'weak' if a.shard == 'samples' else 'strong',
         'vs_baseline': None,
         'dtype': 'f32',
         'data': 'reference scene vol2_final_scene compiled at random.seed(1234) (tests/golden fixture); '
@@ -186,8 +187,8 @@ def main():
             'workload': f'{a.scene} {W}x{H}, {"wavefront" if a.variant == "wf" else "megakernel"} integrator, '
                         f'{sps * a.steps} spp per GPU ({a.steps} steps x {sps} spp), max_depth {a.max_depth}',
             'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'spp_per_step': sps,
-            'spp_per_gpu': sps * a.steps, 'max_depth': a.max_depth, 'seed': a.seed,
-            'parallelism': f'sample-shard x{world} + RCCL reduce' if world > 1 else 'single GPU',
+            'spp_per_gpu': sps * a.steps if a.shard == 'samples' else f'{sps * a.steps} (rows 1/{world})', 'max_depth': a.max_depth, 'seed': a.seed,
+            'parallelism': (f'{a.shard}-shard x{world} + RCCL reduce' if world > 1 else 'single GPU'),
         },
         'roofline': {
             'bound': 'hbm', 'kernel': dom,

@@ -139,8 +139,9 @@ PT_HD float pt_atan_pos(float x) {
     return y0 + fmaf(p * z, t, t);
 }
 PT_HD float pt_atanf(float x) {
-    float a = pt_atan_pos(x < 0.0f ? -x : x);
-    return (x < 0.0f) ? -a : a;
+    uint32_t sb = pt_f2u_bits(x) & 0x80000000u;
+    float a = pt_atan_pos(pt_u2f_bits(pt_f2u_bits(x) & 0x7fffffffu));
+    return pt_u2f_bits(pt_f2u_bits(a) ^ sb);  /* odd, incl. signed zero */
 }
 /* atan2 with IEEE signed-zero conventions for the y = +-0 cases. */
 PT_HD float pt_atan2f(float y, float x) {

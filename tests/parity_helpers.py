@@ -18,13 +18,14 @@ def fixture(name):
     return _cache[name]
 
 
-def oracle_render(name, width, variant, window, s_begin, s_count, seed=0, max_depth=50, threads=0):
+def oracle_render(name, width, variant, window, s_begin, s_count, seed=0, max_depth=50, threads=0, acc=None):
     import oracle
     sa = fixture(name)
     cam = sd.fixture_camera(name, width)
     W, H = cam['width'], cam['height']
     fr = oracle.make_frame(cam, BG[name], max_depth, seed, W, H)
-    acc = np.zeros((H, W, 3), np.float32)
+    if acc is None:
+        acc = np.zeros((H, W, 3), np.float32)
     stats = oracle.render(oracle.OracleScene(sa), fr, variant, acc, window, s_begin, s_count, threads)
     return acc, stats
 

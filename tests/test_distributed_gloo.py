@@ -1,0 +1,66 @@
+"""World-size-2 multi-process test of the multi-GPU partition on CPU (gloo).
+
+Each rank renders its shard with the CPU oracle standing in for its GPU (the
+kernels themselves are covered by the -m gpu parity tests) and the product's
+ptmi.distributed.reduce_accum assembles the image on rank 0:
+  * tiles   -> bit-identical to the single-device render,
+  * samples -> equal up to f32 summation order.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCENE, WIDTH, SPS, STEPS = 'vol2_final_scene', 64, 2, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, mode, out_path):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, 'path-tracer-python_amd'), os.path.join(ROOT, 'tests')):
+        sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from parity_helpers import oracle_render
+    from ptmi import device
+    from ptmi.distributed import Shard, reduce_accum
+    sh = Shard(rank, world, mode, band_rows=8)
+    H = WIDTH
+    acc = np.zeros((H, WIDTH, 3), np.float32)
+    rows = sh.rows(H)
+    for k in range(STEPS):
+        b, c = sh.sample_range(k, SPS)
+        # render exactly the rows the frame's band selects
+        for r in rows:  # accumulate in place: same per-pixel float order as one device
+            oracle_render(SCENE, WIDTH, 'mk', (0, r, WIDTH, 1), b, c, threads=1, acc=acc)
+    t = torch.from_numpy(acc)
+    reduce_accum(t, dst=0)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('mode', ['tiles', 'samples'])
+def test_two_rank_partition(tmp_path, mode):
+    from parity_helpers import oracle_render
+    out = str(tmp_path / f'{mode}.npy')
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, start_method='spawn')
+    got = np.load(out)
+    spp_total = SPS * STEPS * (2 if mode == 'samples' else 1)
+    ref, _ = oracle_render(SCENE, WIDTH, 'mk', (0, 0, WIDTH, WIDTH), 0, spp_total)
+    if mode == 'tiles':
+        assert np.array_equal(got, ref, equal_nan=True)
+    else:
+        assert np.allclose(got / spp_total, ref / spp_total, rtol=1e-5, atol=1e-6, equal_nan=True)

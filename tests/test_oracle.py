@@ -1,0 +1,118 @@
+"""CPU tests of the oracle itself: closest-hit traversal against a brute-force
+scan, and BASELINE config 1 (wavefront_comparison 400x225 @ 4 spp, the
+reference's ti.cpu plumbing case) end to end on the CPU."""
+import numpy as np
+import pytest
+
+import oracle
+from parity_helpers import BG, fixture, oracle_render
+from ptmi import scene_data as sd
+
+
+def dot(a, b):
+    """(x + y) + z in f32, the contract's dot (no BLAS/FMA reordering)."""
+    return np.float32(np.float32(a[0] * b[0]) + np.float32(a[1] * b[1])) + np.float32(a[2] * b[2])
+
+
+def cross(a, b):
+    return np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]], np.float32)
+
+
+def brute_force(sa, o, d, tmin=np.float32(0.001), tmax=np.float32(1e10)):
+    """Closest hit over every primitive with the reference formulas (f32)."""
+    best_t, best = tmax, (-1, -1)
+    for i, s in enumerate(sa.sphere_data):
+        c, r = s[:3], s[3]
+        oc = c - o
+        a = dot(d, d)
+        h = dot(d, oc)
+        cc = dot(oc, oc) - r * r
+        disc = h * h - a * cc
+        if disc >= 0:
+            sq = np.sqrt(disc)
+            for root in ((h - sq) / a, (h + sq) / a):
+                if tmin <= root <= tmax:
+                    if root < best_t:
+                        best_t, best = root, (0, i)
+                    break
+    q = sa.quads
+    for i in range(sa.num_quads):
+        n = q['quad_normal'][i]
+        den = dot(n, d)
+        if abs(den) >= 1e-8:
+            t = (q['quad_D'][i] - dot(n, o)) / den
+            if tmin <= t <= tmax:
+                p = (o + t * d) - q['quad_Q'][i]
+                w = q['quad_w'][i]
+                al = dot(w, cross(p, q['quad_v'][i]))
+                be = dot(w, cross(q['quad_u'][i], p))
+                if 0 <= al <= 1 and 0 <= be <= 1 and t < best_t:
+                    best_t, best = t, (2, i)
+    return best_t, best
+
+
+@pytest.mark.parametrize('name', ['wavefront_comparison', 'cornell_smoke'])
+def test_traversal_matches_brute_force(name):
+    sa = fixture(name)
+    osc = oracle.OracleScene(sa)
+    rng = np.random.default_rng(5)
+    cam = sd.fixture_camera(name, 800)
+    agree = 0
+    n = 300
+    for _ in range(n):
+        o = cam['center'] + rng.normal(0, 0.5, 3).astype(np.float32)
+        d = (cam['pixel00'] + rng.uniform(0, 800) * cam['delta_u'] + rng.uniform(0, cam['height']) * cam['delta_v']
+             - o).astype(np.float32)
+        hit, t, ty, ix = oracle.traverse(osc, o, d)
+        bt, (bty, bix) = brute_force(sa, o.astype(np.float32), d)
+        if bty < 0:
+            assert not hit
+            agree += 1
+        else:
+            assert hit
+            assert t == bt
+            agree += (ty, ix) == (bty, bix)
+    assert agree >= n - 2  # exact float ties may resolve differently
+
+
+@pytest.fixture(scope='module')
+def config1():
+    """BASELINE configs[0]: wavefront_comparison 400x225 @ 4 spp, both variants."""
+    out = {}
+    for v in ('mk', 'wf'):
+        out[v] = oracle_render('wavefront_comparison', 400, v, (0, 0, 400, 225), 0, 4)
+    return out
+
+
+def test_config1_plumbing(config1):
+    for v, (acc, st) in config1.items():
+        img = acc / 4
+        assert np.isfinite(img).all()
+        assert st['paths'] == 400 * 225 * 4
+        assert 1.5 < st['segments'] / st['paths'] < 3.5
+        assert 0.3 < img.mean() < 0.7
+        # sky (bg 0.7,0.8,1.0) dominates the top rows
+        top = img[:20].reshape(-1, 3).mean(0)
+        assert top[2] > top[0]
+
+
+def test_config1_megakernel_vs_wavefront_statistically_equal(config1):
+    """Q1/Q11/Q14 make the variants differ per path, not in expectation."""
+    a = config1['mk'][0] / 4
+    b = config1['wf'][0] / 4
+    ca, cb = a.reshape(-1, 3).mean(0), b.reshape(-1, 3).mean(0)
+    assert np.all(np.abs(ca - cb) < 0.01)
+    # blurred images agree
+    k = 25
+    ba = a[:225 // k * k, :400 // k * k].reshape(225 // k, k, 400 // k, k, 3).mean((1, 3))
+    bb = b[:225 // k * k, :400 // k * k].reshape(225 // k, k, 400 // k, k, 3).mean((1, 3))
+    assert np.max(np.abs(ba - bb)) < 0.08
+
+
+def test_oracle_deterministic_and_window_local():
+    a, _ = oracle_render('vol2_final_scene', 64, 'mk', (8, 8, 16, 16), 0, 3)
+    b, _ = oracle_render('vol2_final_scene', 64, 'mk', (8, 8, 16, 16), 0, 3, threads=1)
+    assert np.array_equal(a, b)
+    full, _ = oracle_render('vol2_final_scene', 64, 'mk', (0, 0, 64, 64), 0, 3)
+    assert np.array_equal(full[8:24, 8:24], a[8:24, 8:24])
+    assert not a[:8].any()
