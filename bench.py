@@ -5,10 +5,11 @@ Metric (BASELINE.json): Msamples/s (+ achieved HBM GB/s) on vol2_final_scene
 800x800 at 1/2/4/8 MI355X. One sample = one camera path for one pixel
 (renderer.py:453-471 prints the same quantity as "M pix/s" at 1 spp/launch).
 
-Workload (BASELINE.json configs[2], the north-star target): vol2_final_scene
-800x800, wavefront integrator, 1024 spp per GPU = --steps 16 x
---spp-per-step 64 by default. A "step" is one call of the hot path over the
-whole image for spp-per-step samples. Scene = the reference's own
+Workload (BASELINE.json configs[1]): vol2_final_scene 800x800, megakernel
+integrator, 64 spp per step; --steps 16 steps by default, i.e. 1024 spp per
+GPU, the sample count of the north-star target (configs[2]; --variant wf runs
+that config's wavefront integrator). A "step" is one call of the hot path
+over the whole image for spp-per-step samples. Scene = the reference's own
 vol2_final_scene compiled arrays captured at random.seed(1234)
 (tests/golden/vol2_final_scene.npz), camera from the reference's camera math.
 
@@ -50,6 +51,10 @@ ALGO_BYTES = {
     'wf_medium': ('medium rays', 108),
     # accumulator read + write, 24 B per pixel per launch
     'megakernel': ('pixel-launches', 24),
+    # camera ray record write, 48 B per ray
+    'wf_generate': ('rays', 48),
+    # accumulator read + write 24 B + batch x 12 B staging read, per pixel
+    'wf_resolve': ('pixels', 24),
 }
 
 
@@ -59,7 +64,7 @@ def parse():
     p.add_argument('--steps', type=int, default=16)
     p.add_argument('--warmup', type=int, default=2)
     p.add_argument('--spp-per-step', type=int, default=64)
-    p.add_argument('--variant', choices=('wf', 'mk'), default='wf')
+    p.add_argument('--variant', choices=('wf', 'mk'), default='mk')
     p.add_argument('--scene', default='vol2_final_scene')
     p.add_argument('--width', type=int, default=800)
     p.add_argument('--max-depth', type=int, default=50)
@@ -161,7 +166,8 @@ def main():
     dom = max((k for k in prof if prof[k]['launches']), key=lambda k: prof[k]['ms'])
     unit_name, unit_bytes = ALGO_BYTES[dom]
     units = {'wf_intersect': cnt['segments'], 'wf_shade': cnt['segments'], 'wf_medium': cnt['medium'],
-             'megakernel': W * rows_rank * prof['megakernel']['launches']}[dom]
+             'megakernel': W * rows_rank * prof['megakernel']['launches'],
+             'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches']}[dom]
     dom_ms = prof[dom]['ms']
     launches = prof[dom]['launches']
     achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0

@@ -116,9 +116,14 @@ int ptmi_mk_render(const ptmi_scene_view *scene, const ptmi_frame *frame, float 
 /* Wavefront: replaces generate_camera_rays / intersect_rays /
  * shade_miss_rays / reset_next_ray_count / shade_and_scatter /
  * swap_ray_buffers (kernels.py:1219-1418) as driven by
- * TaichiRenderer.render_wavefront() (renderer.py:305-334). workspace must be
- * ptmi_wf_workspace_bytes(frame) bytes of device memory (16-byte aligned). */
-size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame);
+ * TaichiRenderer.render_wavefront() (renderer.py:305-334), with the same
+ * accumulation semantics as ptmi_mk_render. workspace: device memory
+ * (16-byte aligned) of at least ptmi_wf_workspace_bytes(frame, 1) bytes;
+ * ptmi_wf_workspace_bytes(frame, B) bytes let one batch hold B samples of
+ * every pixel (ray queues + a per-(sample, pixel) staging slot). Larger
+ * sample counts run in batches. Synchronises the stream once every few
+ * queue iterations to read the live-ray count (not graph-capturable). */
+size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
                    uint64_t *counters, void *stream);
@@ -148,9 +153,10 @@ int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int
  * ptmi_prof_start pre-creates events for max_launches launches; render calls
  * then record around every kernel; ptmi_prof_stop synchronises, returns the
  * summed milliseconds and launch counts per kernel kind
- * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 wf_shade, 4 wf_medium}
- * and disables timing. Not thread-safe; one profiling session per process. */
-#define PTMI_PROF_KINDS 5
+ * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 wf_shade, 4 wf_medium,
+ * 5 wf_resolve} and disables timing. Not thread-safe; one profiling session
+ * per process. */
+#define PTMI_PROF_KINDS 6
 int ptmi_prof_start(int32_t max_launches);
 int ptmi_prof_stop(double *ms_by_kernel, uint64_t *launches_by_kernel, int32_t n_kinds);
 

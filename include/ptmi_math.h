@@ -52,10 +52,18 @@ PT_HD pt_v3 pt_cross(pt_v3 a, pt_v3 b) {
 /* Taichi Matrix.normalized(): v * (1 / sqrt(v.dot(v)))  (SURVEY.md Q31). */
 PT_HD pt_v3 pt_normalize(pt_v3 a) { float inv = 1.0f / sqrtf(pt_dot(a, a)); return pt_scale(a, inv); }
 
-/* ti.min / ti.max on non-NaN operands; written as selects so both compilers
- * lower them identically (NaN: returns the second operand). */
+/* ti.min / ti.max. Default: IEEE-754 minNum/maxNum (fminf/fmaxf: a NaN
+ * operand yields the other operand), which gfx950 executes as one
+ * v_min/v_max(3)_f32 and glibc implements identically; PTMI_SELECT_MINMAX
+ * selects the compare-and-select form instead. The integrator never feeds
+ * these a signed-zero pair whose sign reaches arithmetic. */
+#ifdef PTMI_SELECT_MINMAX
 PT_HD float pt_minf(float a, float b) { return (a < b) ? a : b; }
 PT_HD float pt_maxf(float a, float b) { return (a > b) ? a : b; }
+#else
+PT_HD float pt_minf(float a, float b) { return fminf(a, b); }
+PT_HD float pt_maxf(float a, float b) { return fmaxf(a, b); }
+#endif
 
 PT_HD uint32_t pt_f2u_bits(float x) { union { float f; uint32_t u; } c; c.f = x; return c.u; }
 PT_HD float pt_u2f_bits(uint32_t u) { union { float f; uint32_t u; } c; c.u = u; return c.f; }

@@ -15,10 +15,10 @@
 namespace ptmi {
 hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, float* accum,
                      int32_t s_begin, int32_t s_count, unsigned long long* counters, hipStream_t stream);
-hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws, int32_t capacity,
+hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws, size_t ws_bytes,
                      float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
                      hipStream_t stream);
-size_t wf_workspace_bytes(int32_t capacity);
+size_t wf_workspace_bytes(int32_t npix, int32_t batch);
 
 // clear_accum_buffer, kernels.py:1205-1209 (restricted to the frame's pixel set).
 __global__ __launch_bounds__(kBlock) void clear_kernel(DevFrame fr, float* __restrict__ accum) {
@@ -186,10 +186,18 @@ int ptmi_mk_render(const ptmi_scene_view* scene, const ptmi_frame* frame, float*
                    "mk_render launch");
 }
 
-size_t ptmi_wf_workspace_bytes(const ptmi_frame* frame) {
+size_t ptmi_wf_workspace_bytes(const ptmi_frame* frame, int32_t batch_samples) {
   DevFrame fr;
   if (to_dev_frame(frame, fr)) return 0;
-  return wf_workspace_bytes(fr.w * fr.n_rows);
+  if (batch_samples <= 0) {
+    fail(PTMI_EINVAL, "batch_samples must be > 0");
+    return 0;
+  }
+  if ((int64_t)fr.w * fr.n_rows * batch_samples > 0x7fffffff) {
+    fail(PTMI_ECAPACITY, "pixels x batch_samples exceeds 2^31 work items");
+    return 0;
+  }
+  return wf_workspace_bytes(fr.w * fr.n_rows, batch_samples);
 }
 
 int ptmi_wf_render(const ptmi_scene_view* scene, const ptmi_frame* frame, void* workspace, size_t workspace_bytes,
@@ -201,13 +209,15 @@ int ptmi_wf_render(const ptmi_scene_view* scene, const ptmi_frame* frame, void* 
   if ((rc = to_dev_frame(frame, fr))) return rc;
   if (!accum) return fail(PTMI_EINVAL, "accum is NULL");
   if (sample_begin < 0 || sample_count < 0) return fail(PTMI_EINVAL, "bad sample range");
-  int32_t cap = fr.w * fr.n_rows;
-  if (!workspace || !aligned16(workspace) || workspace_bytes < wf_workspace_bytes(cap))
-    return fail(PTMI_EINVAL, "workspace too small/misaligned (%zu < %zu)", workspace_bytes, wf_workspace_bytes(cap));
-  if (sample_count == 0 || cap == 0) return PTMI_OK;
-  return check_hip(wf_render(sc, fr, stack_needed(scene), workspace, cap, accum, sample_begin, sample_count,
-                             (unsigned long long*)counters, (hipStream_t)stream),
-                   "wf_render launch");
+  int32_t npix = fr.w * fr.n_rows;
+  if (npix == 0) return PTMI_OK;
+  if (!workspace || !aligned16(workspace) || workspace_bytes < wf_workspace_bytes(npix, 1))
+    return fail(PTMI_EINVAL, "workspace too small/misaligned (%zu < %zu)", workspace_bytes,
+                wf_workspace_bytes(npix, 1));
+  if (sample_count == 0) return PTMI_OK;
+  return check_hip(wf_render(sc, fr, stack_needed(scene), workspace, workspace_bytes, accum, sample_begin,
+                             sample_count, (unsigned long long*)counters, (hipStream_t)stream),
+                   "wf_render");
 }
 
 int ptmi_clear(const ptmi_frame* frame, float* accum, void* stream) {

@@ -225,15 +225,101 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // t < closest_t. Each stack entry carries the child's slab entry distance E
 // (computed once when the parent is expanded); the reference's pop-time
 // test max(E, t_min) <= min(X, closest_t) is split exactly into X >= E (at
-// push) and E <= closest_t (at pop). Stack: STACK slots per thread in LDS,
-// slot-major so a wave's 64 lanes hit 64 distinct banks.
+// push) and E <= closest_t (at pop). The near child is not pushed and popped
+// again: it is taken directly (same test, same closest_t), so only far
+// children touch the stack. Stack: STACK 8-byte {ref, E} slots per thread in
+// LDS, slot-major, so a wave's ds_read_b64/ds_write_b64 hit distinct banks.
 
 struct Stack {
-  uint32_t* ref;  // &lds_ref[tid]
-  float* te;      // &lds_t[tid]
+  uint2* slot0;  // &lds[tid]; slot k at slot0[k * kBlock]
 };
 
-__device__ __forceinline__ void child_slab(float4 lo_a, pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz,
+__device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz, float mxx, float mxy,
+                                     float mxz, float tmin, float& E, float& X) {
+  float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
+  float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
+  float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
+  E = pt_maxf(pt_maxf(pt_minf(t0x, t1x), pt_minf(t0y, t1y)), pt_maxf(pt_minf(t0z, t1z), tmin));
+  X = pt_minf(pt_minf(pt_maxf(t0x, t1x), pt_maxf(t0y, t1y)), pt_maxf(t0z, t1z));
+}
+
+template <int STACK>
+__device__ __forceinline__ bool traverse_v2(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
+                                            Stack st, float& t_out, int32_t& ref_out) {
+  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  float closest = tmax;
+  int32_t best = 0;
+  bool any = false;
+  if (sc.n_inner == 0 && sc.root_ref >= 0) {  // empty scene
+    t_out = tmax;
+    ref_out = 0;
+    return false;
+  }
+  int sp = 0;
+  int32_t cur = sc.root_ref;
+  bool have;
+  {
+    float E, X;
+    slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
+         tmin, E, X);
+    have = pt_minf(X, closest) >= E;
+  }
+  while (have) {
+    if (cur < 0) {  // leaf: kernels.py:671-697
+      float t;
+      if (hit_leaf(sc, cur, o, d, tmin, closest, t) && t < closest) {
+        closest = t;
+        best = cur;
+        any = true;
+      }
+    } else {  // internal: kernels.py:698-740
+      const float4* nd = sc.nodes + 4 * cur;
+      const float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+      float E0, X0, E1, X1;
+      slab(o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
+      slab(o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
+      pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
+      pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
+      const bool left_near = pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d);
+      const int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+      const int32_t nr = left_near ? r0 : r1, fr = left_near ? r1 : r0;
+      const float nE = left_near ? E0 : E1, fE = left_near ? E1 : E0;
+      const bool nh = left_near ? (X0 >= E0) : (X1 >= E1);
+      const bool fh = left_near ? (X1 >= E1) : (X0 >= E0);
+      if (nh && nE <= closest) {
+        if (fh && sp < STACK) {
+          st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+          ++sp;
+        }
+        cur = nr;
+        continue;
+      }
+      if (fh && fE <= closest) {
+        cur = fr;
+        continue;
+      }
+    }
+    have = false;  // pop the next live entry
+    while (sp > 0) {
+      --sp;
+      const uint2 ent = st.slot0[sp * kBlock];
+      if (__uint_as_float(ent.y) <= closest) {
+        cur = (int32_t)ent.x;
+        have = true;
+        break;
+      }
+    }
+  }
+  t_out = closest;
+  ref_out = best;
+  return any;
+}
+
+// Variant without the near-child shortcut (every child pushed), kept for A/B
+// timing (PTMI_TRAVERSAL=1).
+
+__device__ __forceinline__ void child_slab_v1(float4 lo_a, pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz,
                                            float mxx, float mxy, float mxz, float tmin, float& E, float& X) {
   float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
   float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
@@ -244,7 +330,7 @@ __device__ __forceinline__ void child_slab(float4 lo_a, pt_v3 o, pt_v3 inv, floa
 }
 
 template <int STACK>
-__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
+__device__ __forceinline__ bool traverse_v1(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
                                          Stack st, float& t_out, int32_t& ref_out) {
   pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
                      fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
@@ -259,18 +345,18 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
   }
   {
     float E, X;
-    child_slab(float4(), o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0],
+    child_slab_v1(float4(), o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0],
                sc.root_max[1], sc.root_max[2], tmin, E, X);
     if (pt_minf(X, closest) >= E) {
-      st.ref[0] = (uint32_t)sc.root_ref;
-      st.te[0] = E;
+      st.slot0[0] = make_uint2((uint32_t)sc.root_ref, __float_as_uint(E));
       sp = 1;
     }
   }
   while (sp > 0) {
     --sp;
-    int32_t ref = (int32_t)st.ref[sp * kBlock];
-    float te = st.te[sp * kBlock];
+    const uint2 ent = st.slot0[sp * kBlock];
+    int32_t ref = (int32_t)ent.x;
+    float te = __uint_as_float(ent.y);
     if (!(te <= closest)) continue;
     if (ref < 0) {
       float t;
@@ -285,8 +371,8 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
     float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
     int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
     float E0, X0, E1, X1;
-    child_slab(a, o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
-    child_slab(a, o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
+    child_slab_v1(a, o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
+    child_slab_v1(a, o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
     pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
     pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
     float ld = pt_dot(pt_sub(lc, o), d);
@@ -296,12 +382,25 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
     int32_t fr = (ld < rd) ? r1 : r0, nr = (ld < rd) ? r0 : r1;
     float fE = (ld < rd) ? E1 : E0, nE = (ld < rd) ? E0 : E1;
     bool fh = (ld < rd) ? h1 : h0, nh = (ld < rd) ? h0 : h1;
-    if (fh && sp < STACK) { st.ref[sp * kBlock] = (uint32_t)fr; st.te[sp * kBlock] = fE; ++sp; }
-    if (nh && sp < STACK) { st.ref[sp * kBlock] = (uint32_t)nr; st.te[sp * kBlock] = nE; ++sp; }
+    if (fh && sp < STACK) { st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE)); ++sp; }
+    if (nh && sp < STACK) { st.slot0[sp * kBlock] = make_uint2((uint32_t)nr, __float_as_uint(nE)); ++sp; }
   }
   t_out = closest;
   ref_out = best;
   return any;
+}
+
+#ifndef PTMI_TRAVERSAL
+#define PTMI_TRAVERSAL 1  // A/B on MI355X: push-both (1) beat the near-child shortcut (2) by 17%
+#endif
+template <int STACK>
+__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
+                                         float& t_out, int32_t& ref_out) {
+#if PTMI_TRAVERSAL == 1
+  return traverse_v1<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
+#else
+  return traverse_v2<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
+#endif
 }
 
 // ---------------------------------------------------------------- textures

@@ -46,16 +46,19 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
   ps.ref_entry = 0;
 }
 
+#ifndef PTMI_MK_MIN_WAVES
+#define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
+#endif
+
 template <int STACK>
-__global__ __launch_bounds__(kBlock) void mk_render_kernel(DevScene sc, DevFrame fr, float* __restrict__ accum,
+__global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(DevScene sc, DevFrame fr, float* __restrict__ accum,
                                                            int32_t s_begin, int32_t s_count,
                                                            unsigned long long* __restrict__ counters) {
-  __shared__ uint32_t lds_ref[STACK * kBlock];
-  __shared__ float lds_t[STACK * kBlock];
+  __shared__ uint2 lds_stack[STACK * kBlock];
   __shared__ unsigned long long blk_cnt[3];
   const int tid = threadIdx.x;
   if (tid < 3) blk_cnt[tid] = 0ull;
-  Stack st{lds_ref + tid, lds_t + tid};
+  Stack st{lds_stack + tid};
 
   // 16x16 pixel block = 4 waves of 8x8 (square footprints keep a wave's
   // camera rays coherent in the BVH).

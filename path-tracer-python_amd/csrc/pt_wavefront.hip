@@ -4,9 +4,8 @@
 // TaichiRenderer.render_wavefront (renderer.py:305-334). Stages and layout
 // are designed for CDNA4, not translated:
 //   * ray queue = three float4 streams per slot (A = o.xyz,d.x;
-//     B = d.yz,thr.xy; C = thr.z, pixel, rng draw counter, meta) so every
-//     load/store is a 16-B-per-lane coalesced access; meta = depth |
-//     wave << 8 | sample << 16 (sample relative to the call's first);
+//     B = d.yz,thr.xy; C = thr.z, work item, rng draw counter, meta) so every
+//     load/store is a 16-B-per-lane coalesced access; meta = depth | wave << 8;
 //   * hit record = 8 B (t, leaf ref); hit point and normal are recomputed in
 //     the shading kernel with the reference's own expressions;
 //   * rays whose closest hit is a constant-medium boundary are compacted into
@@ -14,17 +13,21 @@
 //     from a dedicated kernel instead of diverging inside shading;
 //   * next-queue append = wave64 ballot + mbcnt prefix + ONE atomic per wave;
 //     ping-pong queues (no swap copy, kernels.py:1402-1418 removed);
-//   * STREAMING: the reference runs one sample at a time through max_depth
-//     bounce-synchronous waves (renderer.py:305-334), so after a few bounces
-//     its queues are nearly empty. Here a path that ends is immediately
-//     replaced in the queue by the camera ray of the same pixel's next
-//     sample, so every launch works on a full queue. Each ray carries its
-//     own wave count and is dropped when it reaches max_depth waves, exactly
-//     the reference's per-path budget (Q14, incl. passthrough waves Q11), and
-//     a pixel's samples still run one after another, so per-path results
-//     and the per-pixel accumulation order are those of the reference loop.
-// Each pixel owns at most one live path at a time, so accumulator updates
-// are plain read-modify-writes (no atomics).
+//   * WORK POOL: the reference pushes one sample of every pixel through
+//     max_depth bounce-synchronous waves (renderer.py:305-334), so after a
+//     few bounces its queues are nearly empty. Here the (sample, pixel) pairs
+//     of a batch are work items handed out by one device counter: whenever a
+//     path ends, its queue slot takes the next item's camera ray, so every
+//     launch works on a full queue until the batch runs out. Each ray carries
+//     its own wave count and is dropped at max_depth waves, exactly the
+//     reference's per-path budget (Q14, incl. passthrough waves Q11).
+//   * A path adds at most one colour to its pixel, when it ends (a miss, or an
+//     emissive hit, which never scatters: kernels.py:1266-1280, 1365-1375,
+//     906), so each path writes that colour (or 0) to a staging slot
+//     [sample][pixel]; a resolve kernel then adds the slots into the
+//     accumulator in sample order — the same float additions, in the same
+//     order, as the reference's per-sample accumulation, with no atomics and
+//     no ordering constraint between concurrent paths of one pixel.
 #include "pt_device.hpp"
 #include "pt_prof.hpp"
 
@@ -33,27 +36,27 @@ namespace ptmi {
 struct Queue {
   float4* a;  // o.xyz, d.x
   float4* b;  // d.y, d.z, thr.x, thr.y
-  float4* c;  // thr.z, pixel, rng counter, meta (bits)
+  float4* c;  // thr.z, item, rng counter, meta (bits)
 };
 
 struct WfBufs {
   Queue q[2];
-  float2* hit;       // t, ref (bits); ref 0x7fffffff = miss
-  int32_t* medq;     // indices into the current queue
-  int32_t* counts;   // [0],[1] queue sizes, [2] medium queue size, [3] pad
-  int32_t capacity;
+  float2* hit;        // t, ref (bits); ref kMissRef = miss
+  int32_t* medq;      // indices into the current queue
+  float* staging;     // [batch][npix][3] path colours
+  int32_t* counts;    // [0],[1] queue sizes, [2] medium queue size, [3] next work item
+  int32_t capacity;   // queue slots
+  int32_t npix;       // pixels of the frame's pixel set
+  int32_t total;      // work items of the current batch (= batch samples * npix)
+  int32_t s_begin;    // first sample of the batch
 };
 
 constexpr int32_t kMissRef = 0x7fffffff;
 
-__device__ __forceinline__ uint32_t pack_meta(int32_t depth, int32_t wave, int32_t srel) {
-  return (uint32_t)depth | ((uint32_t)wave << 8) | ((uint32_t)srel << 16);
-}
-
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
-// Wave-aggregated append: returns this lane's slot (meaningful only if want).
-__device__ __forceinline__ int32_t wave_append(bool want, int32_t* counter) {
+// Wave-aggregated counter increment: this lane's ticket (meaningful only if want).
+__device__ __forceinline__ int32_t wave_ticket(bool want, int32_t* counter) {
   unsigned long long mask = __ballot(want);
   if (mask == 0ull) return -1;
   int32_t prefix = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -73,13 +76,13 @@ __device__ __forceinline__ void wave_count(bool flag, unsigned long long* counte
 
 struct Ray {
   pt_v3 o, d, thr;
-  uint32_t pixel, ctr, meta;
+  uint32_t item, ctr, meta;
 };
 
 __device__ __forceinline__ void store_ray(const Queue& q, int32_t i, const Ray& r) {
   q.a[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
   q.b[i] = make_float4(r.d.y, r.d.z, r.thr.x, r.thr.y);
-  q.c[i] = make_float4(r.thr.z, __uint_as_float(r.pixel), __uint_as_float(r.ctr), __uint_as_float(r.meta));
+  q.c[i] = make_float4(r.thr.z, __uint_as_float(r.item), __uint_as_float(r.ctr), __uint_as_float(r.meta));
 }
 
 __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
@@ -88,45 +91,60 @@ __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
   r.o = pt_v3f(a.x, a.y, a.z);
   r.d = pt_v3f(a.w, b.x, b.y);
   r.thr = pt_v3f(b.z, b.w, c.x);
-  r.pixel = __float_as_uint(c.y);
+  r.item = __float_as_uint(c.y);
   r.ctr = __float_as_uint(c.z);
   r.meta = __float_as_uint(c.w);
   return r;
 }
 
-__device__ __forceinline__ void accum_add(float* __restrict__ accum, uint32_t pixel, pt_v3 v) {
-  float* p = accum + 3 * (size_t)pixel;
-  p[0] += v.x;
-  p[1] += v.y;
-  p[2] += v.z;
+// Work item k -> (sample, image pixel): sample-major, pixels row-major over
+// the frame's pixel set.
+struct Item {
+  int32_t srel, p, px, py;
+};
+__device__ __forceinline__ Item decode_item(const DevFrame& fr, const WfBufs& wb, uint32_t k) {
+  Item it;
+  it.srel = (int32_t)(k / (uint32_t)wb.npix);
+  it.p = (int32_t)(k - (uint32_t)it.srel * (uint32_t)wb.npix);
+  int32_t lr = it.p / fr.w;
+  it.px = fr.x0 + (it.p - lr * fr.w);
+  it.py = frame_row(fr, lr);
+  return it;
+}
+
+__device__ __forceinline__ uint32_t path_key(const DevFrame& fr, const WfBufs& wb, const Item& it) {
+  return pt_path_key(fr.seed, (uint32_t)(it.py * fr.width + it.px), (uint32_t)(wb.s_begin + it.srel));
 }
 
 // generate_camera_rays, kernels.py:1219-1239 (direction left unnormalized, Q1).
-__device__ __forceinline__ Ray camera_ray(const DevFrame& fr, uint32_t pixel, int32_t s_begin, int32_t srel) {
-  int32_t py = (int32_t)(pixel / (uint32_t)fr.width);
-  int32_t px = (int32_t)(pixel - (uint32_t)py * (uint32_t)fr.width);
-  Rng rng{pt_path_key(fr.seed, pixel, (uint32_t)(s_begin + srel)), 0u};
+__device__ __forceinline__ Ray camera_ray(const DevFrame& fr, const WfBufs& wb, uint32_t k) {
+  Item it = decode_item(fr, wb, k);
+  Rng rng{path_key(fr, wb, it), 0u};
   Ray r;
-  get_ray(fr, px, py, rng, r.o, r.d);
+  get_ray(fr, it.px, it.py, rng, r.o, r.d);
   r.thr = pt_v3f(1.0f, 1.0f, 1.0f);
-  r.pixel = pixel;
+  r.item = k;
   r.ctr = rng.n;
-  r.meta = pack_meta(0, 0, srel);
+  r.meta = 0u;
   return r;
 }
 
-__global__ __launch_bounds__(kBlock) void wf_generate(DevFrame fr, WfBufs wb, int32_t s_begin) {
-  const int32_t npix = fr.w * fr.n_rows;
-  for (int32_t i = (int32_t)(blockIdx.x * kBlock + threadIdx.x); i < npix; i += (int32_t)(gridDim.x * kBlock)) {
-    int32_t lr = i / fr.w;
-    int32_t px = fr.x0 + (i - lr * fr.w);
-    int32_t py = frame_row(fr, lr);
-    store_ray(wb.q[0], i, camera_ray(fr, (uint32_t)(py * fr.width + px), s_begin, 0));
-  }
+__device__ __forceinline__ void stage(const WfBufs& wb, uint32_t k, pt_v3 c) {
+  float* p = wb.staging + 3 * (size_t)k;
+  p[0] = c.x;
+  p[1] = c.y;
+  p[2] = c.z;
+}
+
+__global__ __launch_bounds__(kBlock) void wf_generate(DevFrame fr, WfBufs wb) {
+  const int32_t n0 = wb.total < wb.capacity ? wb.total : wb.capacity;
+  for (int32_t i = (int32_t)(blockIdx.x * kBlock + threadIdx.x); i < n0; i += (int32_t)(gridDim.x * kBlock))
+    store_ray(wb.q[0], i, camera_ray(fr, wb, (uint32_t)i));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    wb.counts[0] = npix;
+    wb.counts[0] = n0;
     wb.counts[1] = 0;
     wb.counts[2] = 0;
+    wb.counts[3] = n0;
   }
 }
 
@@ -134,10 +152,9 @@ __global__ __launch_bounds__(kBlock) void wf_generate(DevFrame fr, WfBufs wb, in
 template <int STACK>
 __global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb, int32_t cur,
                                                        unsigned long long* __restrict__ counters) {
-  __shared__ uint32_t lds_ref[STACK * kBlock];
-  __shared__ float lds_t[STACK * kBlock];
+  __shared__ uint2 lds_stack[STACK * kBlock];
   const int tid = threadIdx.x;
-  Stack st{lds_ref + tid, lds_t + tid};
+  Stack st{lds_stack + tid};
   const int32_t n = wb.counts[cur];
   if (blockIdx.x == 0 && tid == 0) {
     wb.counts[cur ^ 1] = 0;  // next queue: last read by the previous iteration's kernels
@@ -155,34 +172,8 @@ __global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb, i
   }
 }
 
-// Continuation of a ray after shading (kernels.py:1377-1399 + the per-path
-// wave budget of renderer.py:313), or regeneration of the pixel's next
-// sample when the path ends.
-struct Next {
-  bool enqueue;
-  bool ended;
-  Ray ray;
-};
-
-__device__ __forceinline__ void continue_or_regen(const DevFrame& fr, int32_t s_begin, int32_t s_count, bool go,
-                                                  const Ray& cont, const Ray& cur, Next& nx) {
-  const int32_t wave = (int32_t)((cur.meta >> 8) & 0xffu);
-  const int32_t srel = (int32_t)(cur.meta >> 16);
-  nx.enqueue = false;
-  nx.ended = false;
-  if (go && wave + 1 < fr.max_depth) {  // waves beyond max_depth are dropped (Q14)
-    nx.enqueue = true;
-    nx.ray = cont;
-    return;
-  }
-  nx.ended = true;
-  if (srel + 1 < s_count) {
-    nx.enqueue = true;
-    nx.ray = camera_ray(fr, cur.pixel, s_begin, srel + 1);
-  }
-}
-
-// scatter epilogue of shade_and_scatter (kernels.py:1377-1391).
+// scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
+// per-path wave budget of renderer.py:313.
 __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scattered, pt_v3 hp, pt_v3 sdir, pt_v3 att,
                                                  const Ray& cur, Rng& r, Ray& out) {
   if (!scattered) return false;
@@ -195,19 +186,33 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
     nthr = pt_divs(nthr, sp);
   }
   int32_t wave = (int32_t)((cur.meta >> 8) & 0xffu);
+  if (wave + 1 >= fr.max_depth) return false;  // Q14: no wave left for the continuation
   out.o = hp;
   out.d = sdir;
   out.thr = nthr;
-  out.pixel = cur.pixel;
+  out.item = cur.item;
   out.ctr = r.n;
-  out.meta = pack_meta(nd, wave + 1, (int32_t)(cur.meta >> 16));
+  out.meta = (uint32_t)nd | ((uint32_t)(wave + 1) << 8);
   return true;
+}
+
+// Per-lane tail of both shading kernels: stage the ended path's colour, take
+// a new work item for the freed slot, and append continuing / new rays.
+__device__ __forceinline__ void finish_lane(const DevFrame& fr, const WfBufs& wb, const Queue& qo, int32_t nxt,
+                                            bool ended, bool go, const Ray& cont,
+                                            unsigned long long* __restrict__ counters) {
+  wave_count(ended, counters ? counters + 2 : nullptr);
+  const int32_t k = wave_ticket(ended, wb.counts + 3);
+  const bool fresh = ended && k < wb.total;
+  const bool want = go || fresh;
+  const int32_t slot = wave_ticket(want, wb.counts + nxt);
+  if (go) store_ray(qo, slot, cont);
+  else if (fresh) store_ray(qo, slot, camera_ray(fr, wb, (uint32_t)k));
 }
 
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
 // medium-boundary hits are compacted into the medium queue.
 __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb, int32_t cur,
-                                                   int32_t s_begin, int32_t s_count, float* __restrict__ accum,
                                                    unsigned long long* __restrict__ counters) {
   const int32_t n = wb.counts[cur];
   const Queue q = wb.q[cur];
@@ -216,41 +221,40 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfB
   const int32_t stride = (int32_t)(gridDim.x * kBlock);
   for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < n; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
-    bool to_medium = false;
-    Next nx;
-    nx.enqueue = false;
-    nx.ended = false;
+    bool to_medium = false, ended = false, go = false;
+    Ray cont;
     if (i < n) {
       const float2 h = wb.hit[i];
       const int32_t ref = __float_as_int(h.y);
       const Ray ray = load_ray(q, i);
-      Ray cont;
-      bool go = false;
       if (ref == kMissRef) {
-        accum_add(accum, ray.pixel, pt_mul(ray.thr, bg));  // shade_miss_rays :1280
+        stage(wb, ray.item, pt_mul(ray.thr, bg));  // shade_miss_rays :1280
+        ended = true;
       } else {
         const int32_t g = mat_index(sc, ref);
         if ((mat_flags(sc, g) >> 8) & 1u) {
           to_medium = true;
         } else {
-          Rng r{pt_path_key(fr.seed, ray.pixel, (uint32_t)(s_begin + (int32_t)(ray.meta >> 16))), ray.ctr};
+          Item it = decode_item(fr, wb, ray.item);
+          Rng r{path_key(fr, wb, it), ray.ctr};
           const Mat m = load_mat(sc, g);
           pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
           pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
           pt_v3 emit = emitted(m);
           pt_v3 sdir, att;
           bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
-          if (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) accum_add(accum, ray.pixel, pt_mul(ray.thr, emit));
           go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
+          if (!go) {
+            ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
+            stage(wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
+                                                                                  : pt_v3f(0.0f, 0.0f, 0.0f));
+          }
         }
       }
-      if (!to_medium) continue_or_regen(fr, s_begin, s_count, go, cont, ray, nx);
     }
-    wave_count(nx.ended, counters ? counters + 2 : nullptr);
-    const int32_t mslot = wave_append(to_medium, wb.counts + 2);
+    const int32_t mslot = wave_ticket(to_medium, wb.counts + 2);
     if (to_medium) wb.medq[mslot] = i;
-    const int32_t slot = wave_append(nx.enqueue, wb.counts + (cur ^ 1));
-    if (nx.enqueue) store_ray(qo, slot, nx.ray);
+    finish_lane(fr, wb, qo, cur ^ 1, ended, go, cont, counters);
   }
 }
 
@@ -259,11 +263,9 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfB
 // (kernels.py:1326-1357).
 template <int STACK>
 __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb, int32_t cur,
-                                                    int32_t s_begin, int32_t s_count, float* __restrict__ accum,
                                                     unsigned long long* __restrict__ counters) {
-  __shared__ uint32_t lds_ref[STACK * kBlock];
-  __shared__ float lds_t[STACK * kBlock];
-  Stack st{lds_ref + threadIdx.x, lds_t + threadIdx.x};
+  __shared__ uint2 lds_stack[STACK * kBlock];
+  Stack st{lds_stack + threadIdx.x};
   const int32_t n = wb.counts[2];
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
   const Queue q = wb.q[cur];
@@ -271,9 +273,8 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
   const int32_t stride = (int32_t)(gridDim.x * kBlock);
   for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < n; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
-    Next nx;
-    nx.enqueue = false;
-    nx.ended = false;
+    bool ended = false, go = false;
+    Ray cont;
     if (j < n) {
       const int32_t i = wb.medq[j];
       const float2 h = wb.hit[i];
@@ -284,40 +285,67 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
       int32_t rex;
       const bool hx = traverse<STACK>(sc, ray.o, ray.d, t_entry + 0.0001f, kTMax, st, te, rex);
       const Mat m = load_mat(sc, mat_index(sc, ref));
-      Rng r{pt_path_key(fr.seed, ray.pixel, (uint32_t)(s_begin + (int32_t)(ray.meta >> 16))), ray.ctr};
+      Item it = decode_item(fr, wb, ray.item);
+      Rng r{path_key(fr, wb, it), ray.ctr};
       float t_exit;
       pt_v3 mp;
-      Ray cont;
-      bool go;
+      pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
       if (medium_step(hx, te, t_entry, m.m3.w, ray.o, ray.d, r, mp, t_exit)) {
         pt_v3 sdir = random_unit_vector(r);
         go = scatter_epilogue(fr, true, mp, sdir, pt_v3f(m.m4.x, m.m4.y, m.m4.z), ray, r, cont);
       } else if (t_exit > 0.0f) {  // passthrough: same depth, next wave (kernels.py:1342-1350)
-        float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
-        cont = ray;
-        cont.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
-        cont.ctr = r.n;
-        cont.meta = ray.meta + (1u << 8);
-        go = true;
+        int32_t wave = (int32_t)((ray.meta >> 8) & 0xffu);
+        if (wave + 1 < fr.max_depth) {
+          float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
+          cont = ray;
+          cont.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
+          cont.ctr = r.n;
+          cont.meta = ray.meta + (1u << 8);
+          go = true;
+        }
       } else {  // fallback (kernels.py:1352-1357)
         pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, t_entry));
         pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
-        pt_v3 emit = emitted(m);
+        emit = emitted(m);
         pt_v3 sdir, att;
         bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
-        if (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) accum_add(accum, ray.pixel, pt_mul(ray.thr, emit));
         go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
       }
-      continue_or_regen(fr, s_begin, s_count, go, cont, ray, nx);
+      if (!go) {
+        ended = true;
+        stage(wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
+                                                                              : pt_v3f(0.0f, 0.0f, 0.0f));
+      }
     }
-    wave_count(nx.ended, counters ? counters + 2 : nullptr);
-    const int32_t slot = wave_append(nx.enqueue, wb.counts + (cur ^ 1));
-    if (nx.enqueue) store_ray(qo, slot, nx.ray);
+    finish_lane(fr, wb, qo, cur ^ 1, ended, go, cont, counters);
   }
 }
 
-static inline unsigned grid_for(int32_t n) {
-  int64_t b = ((int64_t)n + kBlock - 1) / kBlock;
+// accum[pixel] += staging[s][p] for s = 0..batch-1 in order (render_sample's
+// per-sample accumulation, kernels.py:1187 / renderer.py:305).
+__global__ __launch_bounds__(kBlock) void wf_resolve(DevFrame fr, WfBufs wb, int32_t batch,
+                                                     float* __restrict__ accum) {
+  for (int32_t p = (int32_t)(blockIdx.x * kBlock + threadIdx.x); p < wb.npix; p += (int32_t)(gridDim.x * kBlock)) {
+    int32_t lr = p / fr.w;
+    int32_t px = fr.x0 + (p - lr * fr.w);
+    int32_t py = frame_row(fr, lr);
+    float* ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
+    float a0 = ap[0], a1 = ap[1], a2 = ap[2];
+    const float* sp = wb.staging + 3 * (size_t)p;
+    for (int32_t s = 0; s < batch; ++s) {
+      const float* c = sp + 3 * (size_t)s * (size_t)wb.npix;
+      a0 += c[0];
+      a1 += c[1];
+      a2 += c[2];
+    }
+    ap[0] = a0;
+    ap[1] = a1;
+    ap[2] = a2;
+  }
+}
+
+static inline unsigned grid_for(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
   if (b < 1) b = 1;
   if (b > 2048) b = 2048;
   return (unsigned)b;
@@ -325,26 +353,44 @@ static inline unsigned grid_for(int32_t n) {
 
 namespace {
 int32_t* g_pinned_count = nullptr;  // host-pinned readback slot for the live-ray count
+constexpr int32_t kMaxCapacity = 1 << 20;
+
+struct Layout {
+  int32_t capacity;
+  size_t q, hit, medq, staging, counts, total;
+};
+
+Layout layout(int32_t npix, int32_t batch) {
+  Layout L;
+  int64_t items = (int64_t)npix * batch;
+  int64_t cap = npix > kMaxCapacity ? npix : kMaxCapacity;
+  if (items < cap) cap = items;
+  if (cap < 1) cap = 1;
+  L.capacity = (int32_t)cap;
+  size_t c = (size_t)cap;
+  L.q = 0;
+  L.hit = L.q + 2 * 3 * sizeof(float4) * c;
+  L.medq = L.hit + sizeof(float2) * c;
+  L.staging = (L.medq + sizeof(int32_t) * c + 15) & ~(size_t)15;
+  L.counts = (L.staging + 3 * sizeof(float) * (size_t)items + 15) & ~(size_t)15;
+  L.total = L.counts + 16 * sizeof(int32_t);
+  return L;
 }
+}  // namespace
 
 template <int STACK>
-static hipError_t wf_run(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, float* accum, int32_t s_begin,
-                         int32_t s_count, unsigned long long* counters, hipStream_t stream) {
-  const int32_t npix = fr.w * fr.n_rows;
-  const unsigned g = grid_for(npix);
-  if (!g_pinned_count) {
-    hipError_t e = hipHostMalloc((void**)&g_pinned_count, sizeof(int32_t), hipHostMallocDefault);
-    if (e != hipSuccess) return e;
-  }
+static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, float* accum, int32_t batch,
+                           unsigned long long* counters, hipStream_t stream) {
+  const unsigned g = grid_for(wb.capacity);
   prof_begin(kProfWfGenerate, stream);
-  hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kBlock), 0, stream, fr, wb, s_begin);
+  hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kBlock), 0, stream, fr, wb);
   prof_end(kProfWfGenerate, stream);
-  // Every path lives at most max_depth waves and a pixel's samples run back
-  // to back, so s_count * max_depth iterations drain every queue.
-  const int64_t max_iters = (int64_t)s_count * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 1;
+  // Each item needs at most max_depth waves and every iteration advances every
+  // live ray by one wave, so total * max_depth iterations always drain the pool.
+  const int64_t max_iters = (int64_t)wb.total * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 1;
   int32_t cur = 0;
   int64_t it = 0;
-  int32_t chunk = 4;
+  int32_t chunk = 8;
   while (it < max_iters) {
     int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
@@ -352,12 +398,10 @@ static hipError_t wf_run(const DevScene& sc, const DevFrame& fr, const WfBufs& w
       hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, wb, cur, counters);
       prof_end(kProfWfIntersect, stream);
       prof_begin(kProfWfShade, stream);
-      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, cur, s_begin, s_count, accum,
-                         counters);
+      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, cur, counters);
       prof_end(kProfWfShade, stream);
       prof_begin(kProfWfMedium, stream);
-      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, cur, s_begin, s_count,
-                         accum, counters);
+      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, cur, counters);
       prof_end(kProfWfMedium, stream);
       cur ^= 1;
     }
@@ -370,41 +414,53 @@ static hipError_t wf_run(const DevScene& sc, const DevFrame& fr, const WfBufs& w
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return e;
     if (*g_pinned_count == 0) break;
-    if (chunk < 16) chunk *= 2;
   }
+  prof_begin(kProfWfResolve, stream);
+  hipLaunchKernelGGL(wf_resolve, dim3(grid_for(wb.npix)), dim3(kBlock), 0, stream, fr, wb, batch, accum);
+  prof_end(kProfWfResolve, stream);
   return hipGetLastError();
 }
 
-size_t wf_workspace_bytes(int32_t capacity) {
-  size_t cap = (size_t)(capacity > 0 ? capacity : 1);
-  size_t q = 3 * sizeof(float4) * cap;
-  return 2 * q + sizeof(float2) * cap + sizeof(int32_t) * cap + 64;
+size_t wf_workspace_bytes(int32_t npix, int32_t batch) {
+  if (npix <= 0 || batch <= 0) return 0;
+  return layout(npix, batch).total;
 }
 
-hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws, int32_t capacity,
+hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws, size_t ws_bytes,
                      float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
                      hipStream_t stream) {
-  char* p = (char*)ws;
-  size_t cap = (size_t)capacity;
-  WfBufs wb;
-  for (int k = 0; k < 2; ++k) {
-    wb.q[k].a = (float4*)p; p += sizeof(float4) * cap;
-    wb.q[k].b = (float4*)p; p += sizeof(float4) * cap;
-    wb.q[k].c = (float4*)p; p += sizeof(float4) * cap;
+  const int32_t npix = fr.w * fr.n_rows;
+  int32_t batch = s_count;
+  while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
+  if (layout(npix, batch).total > ws_bytes) return hipErrorInvalidValue;
+  if (!g_pinned_count) {
+    hipError_t e = hipHostMalloc((void**)&g_pinned_count, sizeof(int32_t), hipHostMallocDefault);
+    if (e != hipSuccess) return e;
   }
-  wb.hit = (float2*)p; p += sizeof(float2) * cap;
-  wb.medq = (int32_t*)p; p += sizeof(int32_t) * cap;
-  p = (char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-  wb.counts = (int32_t*)p;
-  wb.capacity = capacity;
-  // sample index relative to the call's first travels in 16 bits of meta
-  for (int32_t b = 0; b < s_count; b += 65535) {
-    int32_t c = s_count - b < 65535 ? s_count - b : 65535;
+  for (int32_t b0 = 0; b0 < s_count; b0 += batch) {
+    const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
+    const Layout L = layout(npix, nb);
+    char* p = (char*)ws;
+    WfBufs wb;
+    size_t c = (size_t)L.capacity;
+    for (int k = 0; k < 2; ++k) {
+      wb.q[k].a = (float4*)(p + L.q + (size_t)(3 * k + 0) * sizeof(float4) * c);
+      wb.q[k].b = (float4*)(p + L.q + (size_t)(3 * k + 1) * sizeof(float4) * c);
+      wb.q[k].c = (float4*)(p + L.q + (size_t)(3 * k + 2) * sizeof(float4) * c);
+    }
+    wb.hit = (float2*)(p + L.hit);
+    wb.medq = (int32_t*)(p + L.medq);
+    wb.staging = (float*)(p + L.staging);
+    wb.counts = (int32_t*)(p + L.counts);
+    wb.capacity = L.capacity;
+    wb.npix = npix;
+    wb.total = npix * nb;
+    wb.s_begin = s_begin + b0;
     hipError_t e;
-    if (stack_needed <= 16) e = wf_run<16>(sc, fr, wb, accum, s_begin + b, c, counters, stream);
-    else if (stack_needed <= 24) e = wf_run<24>(sc, fr, wb, accum, s_begin + b, c, counters, stream);
-    else if (stack_needed <= 32) e = wf_run<32>(sc, fr, wb, accum, s_begin + b, c, counters, stream);
-    else e = wf_run<64>(sc, fr, wb, accum, s_begin + b, c, counters, stream);
+    if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wb, accum, nb, counters, stream);
+    else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wb, accum, nb, counters, stream);
+    else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wb, accum, nb, counters, stream);
+    else e = wf_batch<64>(sc, fr, wb, accum, nb, counters, stream);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

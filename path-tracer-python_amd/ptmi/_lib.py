@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, '_lib', 'libptmi.so')
+LIB_PATH = os.environ.get('PTMI_LIB') or os.path.join(_HERE, '_lib', 'libptmi.so')  # PTMI_LIB: A/B builds
 MAX_IMAGES = 16
 NUM_COUNTERS = 4
 
@@ -47,7 +47,7 @@ class Frame(C.Structure):
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
            'ptmi_prof_stop')
-PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium')
+PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve')
 
 _lib = None
 
@@ -70,7 +70,7 @@ def load(path: str = LIB_PATH):
     lib.ptmi_last_error.restype = C.c_char_p
     lib.ptmi_scene_check.argtypes = [C.POINTER(SceneView)]
     lib.ptmi_mk_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_int32, C.c_int32, P, P]
-    lib.ptmi_wf_workspace_bytes.argtypes = [C.POINTER(Frame)]
+    lib.ptmi_wf_workspace_bytes.argtypes = [C.POINTER(Frame), C.c_int32]
     lib.ptmi_wf_workspace_bytes.restype = C.c_size_t
     lib.ptmi_wf_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,
                                    C.c_int32, P, P]

@@ -138,8 +138,13 @@ class Integrator:
                                            int(sample_begin), int(sample_count), self._cnt(), _stream_ptr(stream)),
                    'ptmi_mk_render')
 
-    def workspace(self, frame):
-        need = int(self.lib.ptmi_wf_workspace_bytes(C.byref(frame)))
+    # staging budget for the wavefront's per-(sample, pixel) colour slots
+    WF_STAGING_BYTES = 1 << 30
+
+    def workspace(self, frame, sample_count=1):
+        npix = frame.w * len(frame_pixel_rows(frame))
+        batch = max(1, min(int(sample_count), self.WF_STAGING_BYTES // max(1, 12 * npix)))
+        need = int(self.lib.ptmi_wf_workspace_bytes(C.byref(frame), batch))
         if need == 0:
             _lib.check(-1, 'ptmi_wf_workspace_bytes')
         if self._ws is None or self._ws_bytes < need:
@@ -149,7 +154,7 @@ class Integrator:
 
     def render_wf(self, frame, accum, sample_begin, sample_count, stream=None):
         _check_accum(accum, frame)
-        ws = self.workspace(frame)
+        ws = self.workspace(frame, sample_count)
         _lib.check(self.lib.ptmi_wf_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(ws.data_ptr()),
                                            self._ws_bytes, C.c_void_p(accum.data_ptr()), int(sample_begin),
                                            int(sample_count), self._cnt(), _stream_ptr(stream)),

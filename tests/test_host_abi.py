@@ -81,7 +81,9 @@ def test_render_rejects_bad_arguments_before_touching_device():
     assert rc == _lib.PTMI_EINVAL and 'accum' in lib.ptmi_last_error().decode()
     rc = lib.ptmi_wf_render(C.byref(v), C.byref(f), None, 0, C.c_void_p(16), 0, 1, None, None)
     assert rc == _lib.PTMI_EINVAL and 'workspace' in lib.ptmi_last_error().decode()
-    assert lib.ptmi_wf_workspace_bytes(C.byref(f)) >= 16 * 8 * 104
+    assert lib.ptmi_wf_workspace_bytes(C.byref(f), 1) >= 16 * 8 * (108 + 12)
+    assert lib.ptmi_wf_workspace_bytes(C.byref(f), 4) - lib.ptmi_wf_workspace_bytes(C.byref(f), 1) >= 3 * 16 * 8 * 12
+    assert lib.ptmi_wf_workspace_bytes(C.byref(f), 0) == 0
 
 
 def test_device_entry_points_fail_loudly_without_gpu():

@@ -21,6 +21,9 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     benchmk) step benchmk 600 python bench.py --variant mk --no-cpu-baseline ;;
     rocprof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 4 --no-cpu-baseline ;;
+    ab) step ab 900 bash tools/gpu_ab.sh ;;
+    counters) step counters 120 rocprofv3 -L ;;
+    pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc -o pass1 -- python tools/ab.py mk 32 1 && step pmc2 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o pass2 -- python tools/ab.py mk 32 1 && step pmc3 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o pass3 -- python tools/ab.py mk 32 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s" ;;
   esac
