@@ -135,7 +135,7 @@ def golden_dir():
 
 def load_earthmap():
     """Decoded RGB8 earthmap (the only image texture the BASELINE scenes use)."""
-    return np.load(os.path.join(golden_dir(), 'earthmap_u8.npz'))['earthmap']
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'assets', 'earthmap_u8.npz'))['earthmap']
 
 
 def load_fixture(name):

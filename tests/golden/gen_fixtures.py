@@ -246,7 +246,7 @@ def main():
         manifest['scenes'][name] = meta
         print(name, meta['num_spheres'], meta['num_quads'], meta['num_triangles'], meta['num_bvh_nodes'])
     if earth is not None:
-        np.savez_compressed(os.path.join(OUT, 'earthmap_u8.npz'), earthmap=earth)
+        np.savez_compressed(os.path.join(OUT, '..', '..', 'path-tracer-python_amd', 'ptmi', 'assets', 'earthmap_u8.npz'), earthmap=earth)
     np.savez_compressed(os.path.join(OUT, 'sah_cases.npz'), **_sah_cases(sah_bvh_builder))
     with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
