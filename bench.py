@@ -49,8 +49,10 @@ ALGO_BYTES = {
     'wf_shade': ('rays', 104),
     # read medium index 4 B + hit 8 B + ray 48 B, write next record 48 B
     'wf_medium': ('medium rays', 108),
-    # accumulator read + write, 24 B per pixel per launch
-    'megakernel': ('pixel-launches', 24),
+    # SURVEY.md §8d graded figure per sample, B_sample = 44 + 24 + 128*S with
+    # S = measured segments/sample: the bytes the reference's stage pipeline
+    # must move for one camera path (the megakernel keeps them in registers)
+    'megakernel': ('samples', None),
     # camera ray record write, 48 B per ray
     'wf_generate': ('rays', 48),
     # accumulator read + write 24 B + batch x 12 B staging read, per pixel
@@ -103,6 +105,26 @@ def cpu_baseline(scene, width, variant, max_depth, seed, budget_s):
             'sample': f'{scene} {W}x{H}, rows {y0}..{y0 + rows - 1} ({W}x{rows} px) x {spp} spp, '
                       f'{"wavefront" if variant == "wf" else "megakernel"} semantics, C oracle '
                       f'(restatement of kernels.py; Taichi ti.cpu absent), {dt:.1f} s'}
+
+
+TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'traffic.json')
+
+
+def measured_traffic(a, kernel):
+    """HBM-side bytes per launch of ``kernel`` from the committed PMC summary
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE per dispatch, gfx950
+    correction of MI355X_MICROARCH.md "HBM"), when it was collected on this
+    exact workload; None otherwise."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    key = f'{a.scene}:{a.width}:{a.variant}:{a.spp_per_step}:{a.max_depth}:{kernel}'
+    r = rows.get(key)
+    if not r:
+        return None
+    return {'bytes_per_launch': r['bytes_per_launch'], 'source': r['source']}
 
 
 def main():
@@ -164,16 +186,19 @@ def main():
 
     prof = kt.result
     dom = max((k for k in prof if prof[k]['launches']), key=lambda k: prof[k]['ms'])
+    S = cnt['segments'] / samples_rank
+    M = cnt['medium'] / samples_rank
+    b_sample = 44 + 24 + 128 * S  # SURVEY.md §8d whole-pipeline algorithmic bytes per sample
     unit_name, unit_bytes = ALGO_BYTES[dom]
+    if unit_bytes is None:
+        unit_bytes = b_sample
     units = {'wf_intersect': cnt['segments'], 'wf_shade': cnt['segments'], 'wf_medium': cnt['medium'],
-             'megakernel': W * rows_rank * prof['megakernel']['launches'],
+             'megakernel': samples_rank,
              'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches']}[dom]
     dom_ms = prof[dom]['ms']
     launches = prof[dom]['launches']
     achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    S = cnt['segments'] / samples_rank
-    M = cnt['medium'] / samples_rank
-    b_sample = 44 + 24 + 128 * S  # SURVEY.md §8d whole-pipeline algorithmic bytes per sample
+    traffic = measured_traffic(a, dom)
 
     out = {
         'metric': METRIC,
@@ -199,9 +224,11 @@ def main():
         'roofline': {
             'bound': 'hbm', 'kernel': dom,
             'achieved': round(achieved, 3), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
-            'frac': round(achieved / HBM_PEAK_GBPS, 6), 'traffic': None,
+            'frac': round(achieved / HBM_PEAK_GBPS, 6),
+            'traffic': traffic['bytes_per_launch'] if traffic else None,
+            'traffic_source': traffic['source'] if traffic else None,
             'algorithmic_bytes_per_launch': round(units * unit_bytes / max(1, launches), 1),
-            'unit_of_work': f'{unit_bytes} B per {unit_name[:-1] if unit_name.endswith("s") else unit_name}',
+            'unit_of_work': f'{unit_bytes:.1f} B per {unit_name[:-1] if unit_name.endswith("s") else unit_name}',
             'avg_launch_ms': round(dom_ms / max(1, launches), 5),
             'launches': launches,
             'timing_truncated': bool(kt.truncated),

@@ -11,16 +11,21 @@
 //   * rays whose closest hit is a constant-medium boundary are compacted into
 //     a separate medium queue and get their exit traversal (kernels.py:417)
 //     from a dedicated kernel instead of diverging inside shading;
-//   * next-queue append = wave64 ballot + mbcnt prefix + ONE atomic per wave;
-//     ping-pong queues (no swap copy, kernels.py:1402-1418 removed);
-//   * WORK POOL: the reference pushes one sample of every pixel through
-//     max_depth bounce-synchronous waves (renderer.py:305-334), so after a
-//     few bounces its queues are nearly empty. Here the (sample, pixel) pairs
-//     of a batch are work items handed out by one device counter: whenever a
-//     path ends, its queue slot takes the next item's camera ray, so every
-//     launch works on a full queue until the batch runs out. Each ray carries
-//     its own wave count and is dropped at max_depth waves, exactly the
-//     reference's per-path budget (Q14, incl. passthrough waves Q11).
+//   * WORK POOL, IN-PLACE SLOTS: the reference pushes one sample of every
+//     pixel through max_depth bounce-synchronous waves (renderer.py:305-334)
+//     and compacts survivors into a next queue with one atomic per ray, so
+//     after a few bounces its queues are nearly empty. Here the (sample,
+//     pixel) pairs of a batch are work items: a queue slot keeps its ray in
+//     place from bounce to bounce (no append, no swap copy: kernels.py:
+//     1402-1418 removed) and, when the path ends, takes the camera ray of the
+//     next work item — so every launch works on a full queue until the batch
+//     runs out. Work-item counters and the medium-queue counters are sharded
+//     8 ways by slot block (blocks b and b+8 share an XCD), with one
+//     wave-aggregated atomic per wave, because a single device-wide counter
+//     saturates near 88 returning atomics/us on MI355X (MI355X_MICROARCH.md,
+//     "dequeue") and was measured at 97 % wait cycles in the shade kernel.
+//     Each ray carries its own wave count and is dropped at max_depth waves,
+//     exactly the reference's per-path budget (Q14, incl. passthrough Q11).
 //   * A path adds at most one colour to its pixel, when it ends (a miss, or an
 //     emissive hit, which never scatters: kernels.py:1266-1280, 1365-1375,
 //     906), so each path writes that colour (or 0) to a staging slot
@@ -33,6 +38,9 @@
 
 namespace ptmi {
 
+constexpr int kShards = 8;
+constexpr uint32_t kDead = 0xffffffffu;  // item of an empty slot
+
 struct Queue {
   float4* a;  // o.xyz, d.x
   float4* b;  // d.y, d.z, thr.x, thr.y
@@ -40,20 +48,38 @@ struct Queue {
 };
 
 struct WfBufs {
-  Queue q[2];
+  Queue q;
   float2* hit;        // t, ref (bits); ref kMissRef = miss
-  int32_t* medq;      // indices into the current queue
+  int32_t* medq;      // kShards segments of medseg slot indices
   float* staging;     // [batch][npix][3] path colours
-  int32_t* counts;    // [0],[1] queue sizes, [2] medium queue size, [3] next work item
-  int32_t capacity;   // queue slots
+  int32_t* ctl;       // kCtlWords counters, one per 256-B line (see ctl_*)
+  int32_t capacity;   // queue slots (multiple of kShards * kBlock)
+  int32_t medseg;     // slots per shard
   int32_t npix;       // pixels of the frame's pixel set
-  int32_t total;      // work items of the current batch (= batch samples * npix)
+  int32_t total;      // work items of the batch (= batch samples * npix)
+  int32_t shard_len;  // items per shard: shard s owns [s*len, min((s+1)*len, total))
   int32_t s_begin;    // first sample of the batch
 };
 
 constexpr int32_t kMissRef = 0x7fffffff;
 
+// Device-scope atomics are performed per cache line at the memory side, so
+// counters sharing a line serialize as one: every counter gets its own
+// 256-B line. Lines 0-7: medium-queue count per shard; 8-15: next work item
+// per shard; 16: live slots (read by the host between chunks).
+constexpr int32_t kLine = 64;
+constexpr int32_t kCtlWords = 17 * kLine;
+__host__ __device__ __forceinline__ int32_t* ctl_medium(const WfBufs& wb, int32_t s) { return wb.ctl + s * kLine; }
+__host__ __device__ __forceinline__ int32_t* ctl_next(const WfBufs& wb, int32_t s) { return wb.ctl + (8 + s) * kLine; }
+__host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl + 16 * kLine; }
+
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// Slot i is processed by block (i / kBlock) % grid, grid a multiple of kShards.
+__device__ __forceinline__ int32_t slot_shard(int32_t i) { return (i / kBlock) % kShards; }
+__device__ __forceinline__ int32_t slot_rank(int32_t i) {  // index of slot i among its shard's slots
+  return ((i / kBlock) / kShards) * kBlock + (i % kBlock);
+}
 
 // Wave-aggregated counter increment: this lane's ticket (meaningful only if want).
 __device__ __forceinline__ int32_t wave_ticket(bool want, int32_t* counter) {
@@ -68,10 +94,18 @@ __device__ __forceinline__ int32_t wave_ticket(bool want, int32_t* counter) {
   return base + prefix;
 }
 
-__device__ __forceinline__ void wave_count(bool flag, unsigned long long* counter) {
+__device__ __forceinline__ void wave_add(bool flag, int32_t* counter, int32_t sign) {
   unsigned long long mask = __ballot(flag);
-  if (counter && mask && lane_id() == __ffsll((long long)mask) - 1)
-    atomicAdd(counter, (unsigned long long)__popcll(mask));
+  if (mask && lane_id() == __ffsll((long long)mask) - 1) atomicAdd(counter, sign * (int32_t)__popcll(mask));
+}
+
+// Statistics counters: each thread tallies in a register over its grid-stride
+// loop; at kernel end the block sums through LDS and adds once.
+__device__ __forceinline__ void block_flush(uint32_t v, unsigned int* lds, unsigned long long* counter) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane_id() == 0 && v) atomicAdd(lds, v);
+  __syncthreads();
+  if (threadIdx.x == 0 && *lds) atomicAdd(counter, (unsigned long long)*lds);
 }
 
 struct Ray {
@@ -83,6 +117,14 @@ __device__ __forceinline__ void store_ray(const Queue& q, int32_t i, const Ray& 
   q.a[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
   q.b[i] = make_float4(r.d.y, r.d.z, r.thr.x, r.thr.y);
   q.c[i] = make_float4(r.thr.z, __uint_as_float(r.item), __uint_as_float(r.ctr), __uint_as_float(r.meta));
+}
+
+__device__ __forceinline__ void kill_slot(const Queue& q, int32_t i) {
+  reinterpret_cast<uint32_t*>(q.c + i)[1] = kDead;
+}
+
+__device__ __forceinline__ uint32_t slot_item(const Queue& q, int32_t i) {
+  return reinterpret_cast<const uint32_t*>(q.c + i)[1];
 }
 
 __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
@@ -136,33 +178,44 @@ __device__ __forceinline__ void stage(const WfBufs& wb, uint32_t k, pt_v3 c) {
   p[2] = c.z;
 }
 
+__device__ __forceinline__ int32_t shard_end(const WfBufs& wb, int32_t s) {
+  int64_t e = (int64_t)(s + 1) * wb.shard_len;
+  return e < wb.total ? (int32_t)e : wb.total;
+}
+
+// Initial fill: the r-th slot of shard s takes item s*shard_len + r.
 __global__ __launch_bounds__(kBlock) void wf_generate(DevFrame fr, WfBufs wb) {
-  const int32_t n0 = wb.total < wb.capacity ? wb.total : wb.capacity;
-  for (int32_t i = (int32_t)(blockIdx.x * kBlock + threadIdx.x); i < n0; i += (int32_t)(gridDim.x * kBlock))
-    store_ray(wb.q[0], i, camera_ray(fr, wb, (uint32_t)i));
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    wb.counts[0] = n0;
-    wb.counts[1] = 0;
-    wb.counts[2] = 0;
-    wb.counts[3] = n0;
+  for (int32_t i = (int32_t)(blockIdx.x * kBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kBlock)) {
+    const int32_t s = slot_shard(i);
+    const int64_t k = (int64_t)s * wb.shard_len + slot_rank(i);
+    const bool live = slot_rank(i) < wb.shard_len && k < shard_end(wb, s);
+    if (live) store_ray(wb.q, i, camera_ray(fr, wb, (uint32_t)k));
+    else kill_slot(wb.q, i);
+    wave_add(live, ctl_live(wb), 1);
+  }
+  if (blockIdx.x < kShards && threadIdx.x == 0) {
+    const int32_t s = (int32_t)blockIdx.x;
+    const int64_t k = (int64_t)s * wb.shard_len + wb.medseg;
+    *ctl_next(wb, s) = (int32_t)(k < shard_end(wb, s) ? k : shard_end(wb, s));
   }
 }
 
 // intersect_rays, kernels.py:1242-1263.
 template <int STACK>
-__global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb, int32_t cur,
+__global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb,
                                                        unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
+  __shared__ unsigned int tally;
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
-  const int32_t n = wb.counts[cur];
-  if (blockIdx.x == 0 && tid == 0) {
-    wb.counts[cur ^ 1] = 0;  // next queue: last read by the previous iteration's kernels
-    wb.counts[2] = 0;
-    if (counters && n > 0) atomicAdd(counters + 0, (unsigned long long)n);
-  }
-  const Queue q = wb.q[cur];
-  for (int32_t i = (int32_t)(blockIdx.x * kBlock + tid); i < n; i += (int32_t)(gridDim.x * kBlock)) {
+  if (tid == 0) tally = 0;
+  if (blockIdx.x < kShards && tid == 0) *ctl_medium(wb, blockIdx.x) = 0;  // medium counts of this iteration
+  __syncthreads();
+  const Queue q = wb.q;
+  uint32_t n_live = 0;
+  for (int32_t i = (int32_t)(blockIdx.x * kBlock + tid); i < wb.capacity; i += (int32_t)(gridDim.x * kBlock)) {
+    if (slot_item(q, i) == kDead) continue;
+    ++n_live;
     float4 a = q.a[i], b = q.b[i];
     pt_v3 o = pt_v3f(a.x, a.y, a.z), d = pt_v3f(a.w, b.x, b.y);
     float t;
@@ -170,6 +223,7 @@ __global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb, i
     bool hit = traverse<STACK>(sc, o, d, kTMin, kTMax, st, t, ref);
     wb.hit[i] = make_float2(t, __int_as_float(hit ? ref : kMissRef));
   }
+  if (counters) block_flush(n_live, &tally, counters + 0);
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
@@ -196,34 +250,48 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
   return true;
 }
 
-// Per-lane tail of both shading kernels: stage the ended path's colour, take
-// a new work item for the freed slot, and append continuing / new rays.
-__device__ __forceinline__ void finish_lane(const DevFrame& fr, const WfBufs& wb, const Queue& qo, int32_t nxt,
-                                            bool ended, bool go, const Ray& cont,
-                                            unsigned long long* __restrict__ counters) {
-  wave_count(ended, counters ? counters + 2 : nullptr);
-  const int32_t k = wave_ticket(ended, wb.counts + 3);
-  const bool fresh = ended && k < wb.total;
-  const bool want = go || fresh;
-  const int32_t slot = wave_ticket(want, wb.counts + nxt);
-  if (go) store_ray(qo, slot, cont);
-  else if (fresh) store_ray(qo, slot, camera_ray(fr, wb, (uint32_t)k));
+// Per-lane tail of both shading kernels: keep a continuing ray in its slot,
+// or give an ended path's slot the next work item of its shard (stealing from
+// the other shards once its own range is spent), or retire the slot.
+__device__ __forceinline__ void finish_lane(const DevFrame& fr, const WfBufs& wb, int32_t i, int32_t shard,
+                                            bool ended, bool go, const Ray& cont) {
+  if (go) store_ray(wb.q, i, cont);
+  bool need = ended;
+  int32_t k = -1;
+  for (int32_t a = 0; a < kShards; ++a) {  // wave-uniform loop (ballot inside)
+    if (__ballot(need) == 0ull) break;
+    const int32_t s = (shard + a) % kShards;
+    const int32_t t = wave_ticket(need, ctl_next(wb, s));
+    if (need && t < shard_end(wb, s)) {
+      k = t;
+      need = false;
+    }
+  }
+  if (ended) {
+    if (k >= 0) store_ray(wb.q, i, camera_ray(fr, wb, (uint32_t)k));
+    else kill_slot(wb.q, i);
+  }
+  wave_add(ended && k < 0, ctl_live(wb), -1);
 }
 
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
-// medium-boundary hits are compacted into the medium queue.
-__global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb, int32_t cur,
+// medium-boundary hits go to their shard's medium queue segment.
+__global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
                                                    unsigned long long* __restrict__ counters) {
-  const int32_t n = wb.counts[cur];
-  const Queue q = wb.q[cur];
-  const Queue qo = wb.q[cur ^ 1];
+  const Queue q = wb.q;
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
   const int32_t stride = (int32_t)(gridDim.x * kBlock);
-  for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < n; base += stride) {
+  const int32_t shard = (int32_t)(blockIdx.x % kShards);
+  __shared__ unsigned int tally;
+  if (threadIdx.x == 0) tally = 0;
+  __syncthreads();
+  uint32_t n_ended = 0;
+  for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < wb.capacity; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
     bool to_medium = false, ended = false, go = false;
     Ray cont;
-    if (i < n) {
+    const bool live = i < wb.capacity && slot_item(q, i) != kDead;
+    if (live) {
       const float2 h = wb.hit[i];
       const int32_t ref = __float_as_int(h.y);
       const Ray ray = load_ray(q, i);
@@ -252,34 +320,49 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfB
         }
       }
     }
-    const int32_t mslot = wave_ticket(to_medium, wb.counts + 2);
-    if (to_medium) wb.medq[mslot] = i;
-    finish_lane(fr, wb, qo, cur ^ 1, ended, go, cont, counters);
+    const int32_t mslot = wave_ticket(to_medium, ctl_medium(wb, shard));
+    if (to_medium) wb.medq[shard * wb.medseg + mslot] = i;
+    finish_lane(fr, wb, i, shard, ended, go, cont);
+    n_ended += ended ? 1u : 0u;
   }
+  if (counters) block_flush(n_ended, &tally, counters + 2);
 }
 
 // Constant-medium rays: exit traversal + free flight (apply_constant_medium,
 // kernels.py:365-450) and the volume branch of shade_and_scatter
-// (kernels.py:1326-1357).
+// (kernels.py:1326-1357). Work index j runs over the concatenated shard segments.
 template <int STACK>
-__global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb, int32_t cur,
+__global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
                                                     unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
+  __shared__ int32_t seg_start[kShards + 1];
+  __shared__ unsigned int tally;
   Stack st{lds_stack + threadIdx.x};
-  const int32_t n = wb.counts[2];
+  if (threadIdx.x == 0) {
+    tally = 0;
+    int32_t acc = 0;
+    for (int s = 0; s < kShards; ++s) {
+      seg_start[s] = acc;
+      acc += *ctl_medium(wb, s);
+    }
+    seg_start[kShards] = acc;
+  }
+  __syncthreads();
+  const int32_t n = seg_start[kShards];
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
-  const Queue q = wb.q[cur];
-  const Queue qo = wb.q[cur ^ 1];
   const int32_t stride = (int32_t)(gridDim.x * kBlock);
+  uint32_t n_ended = 0;
   for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < n; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
     Ray cont;
+    int32_t i = -1, shard = 0;
     if (j < n) {
-      const int32_t i = wb.medq[j];
+      while (shard + 1 < kShards && j >= seg_start[shard + 1]) ++shard;
+      i = wb.medq[shard * wb.medseg + (j - seg_start[shard])];
       const float2 h = wb.hit[i];
       const int32_t ref = __float_as_int(h.y);
-      const Ray ray = load_ray(q, i);
+      const Ray ray = load_ray(wb.q, i);
       const float t_entry = h.x;
       float te;
       int32_t rex;
@@ -317,8 +400,12 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
                                                                               : pt_v3f(0.0f, 0.0f, 0.0f));
       }
     }
-    finish_lane(fr, wb, qo, cur ^ 1, ended, go, cont, counters);
+    // refill from the block's shard: the segment shard varies across a wave,
+    // and the ticket counter must be wave-uniform
+    finish_lane(fr, wb, i, (int32_t)(blockIdx.x % kShards), ended, go, cont);
+    n_ended += ended ? 1u : 0u;
   }
+  if (counters) block_flush(n_ended, &tally, counters + 2);
 }
 
 // accum[pixel] += staging[s][p] for s = 0..batch-1 in order (render_sample's
@@ -344,20 +431,17 @@ __global__ __launch_bounds__(kBlock) void wf_resolve(DevFrame fr, WfBufs wb, int
   }
 }
 
-static inline unsigned grid_for(int64_t n) {
-  int64_t b = (n + kBlock - 1) / kBlock;
-  if (b < 1) b = 1;
-  if (b > 2048) b = 2048;
-  return (unsigned)b;
-}
-
 namespace {
-int32_t* g_pinned_count = nullptr;  // host-pinned readback slot for the live-ray count
-constexpr int32_t kMaxCapacity = 1 << 20;
+int32_t* g_pinned_live = nullptr;  // host-pinned readback slot for the live-slot count
+#ifndef PTMI_WF_CAPACITY_LOG2
+#define PTMI_WF_CAPACITY_LOG2 20
+#endif
+constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
+constexpr int32_t kSlotQuantum = kShards * kBlock;
 
 struct Layout {
-  int32_t capacity;
-  size_t q, hit, medq, staging, counts, total;
+  int32_t capacity, medseg;
+  size_t q, hit, medq, staging, ctl, total;
 };
 
 Layout layout(int32_t npix, int32_t batch) {
@@ -365,15 +449,16 @@ Layout layout(int32_t npix, int32_t batch) {
   int64_t items = (int64_t)npix * batch;
   int64_t cap = npix > kMaxCapacity ? npix : kMaxCapacity;
   if (items < cap) cap = items;
-  if (cap < 1) cap = 1;
+  cap = (cap + kSlotQuantum - 1) / kSlotQuantum * kSlotQuantum;
   L.capacity = (int32_t)cap;
+  L.medseg = (int32_t)(cap / kShards);
   size_t c = (size_t)cap;
   L.q = 0;
-  L.hit = L.q + 2 * 3 * sizeof(float4) * c;
+  L.hit = L.q + 3 * sizeof(float4) * c;
   L.medq = L.hit + sizeof(float2) * c;
   L.staging = (L.medq + sizeof(int32_t) * c + 15) & ~(size_t)15;
-  L.counts = (L.staging + 3 * sizeof(float) * (size_t)items + 15) & ~(size_t)15;
-  L.total = L.counts + 16 * sizeof(int32_t);
+  L.ctl = (L.staging + 3 * sizeof(float) * (size_t)items + 255) & ~(size_t)255;
+  L.total = L.ctl + kCtlWords * sizeof(int32_t);
   return L;
 }
 }  // namespace
@@ -381,42 +466,49 @@ Layout layout(int32_t npix, int32_t batch) {
 template <int STACK>
 static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, float* accum, int32_t batch,
                            unsigned long long* counters, hipStream_t stream) {
-  const unsigned g = grid_for(wb.capacity);
+#ifdef PTMI_WF_NOCOUNT
+  counters = nullptr;  // A/B only: prices the statistics atomics
+#endif
+  // grid = multiple of kShards and of the slot quantum, so slot i always maps
+  // to block (i / kBlock) % grid with shard (i / kBlock) % kShards
+  int64_t blocks = wb.capacity / kBlock;
+  if (blocks > 2048) blocks = 2048;
+  const unsigned g = (unsigned)blocks;
+  (void)hipMemsetAsync(wb.ctl, 0, kCtlWords * sizeof(int32_t), stream);
   prof_begin(kProfWfGenerate, stream);
   hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kBlock), 0, stream, fr, wb);
   prof_end(kProfWfGenerate, stream);
   // Each item needs at most max_depth waves and every iteration advances every
   // live ray by one wave, so total * max_depth iterations always drain the pool.
   const int64_t max_iters = (int64_t)wb.total * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 1;
-  int32_t cur = 0;
   int64_t it = 0;
-  int32_t chunk = 8;
+  const int32_t chunk = 8;
   while (it < max_iters) {
     int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
       prof_begin(kProfWfIntersect, stream);
-      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, wb, cur, counters);
+      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, wb, counters);
       prof_end(kProfWfIntersect, stream);
       prof_begin(kProfWfShade, stream);
-      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, cur, counters);
+      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, counters);
       prof_end(kProfWfShade, stream);
       prof_begin(kProfWfMedium, stream);
-      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, cur, counters);
+      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, counters);
       prof_end(kProfWfMedium, stream);
-      cur ^= 1;
     }
     it += n;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // live-ray count of the queue the next iteration would consume
-    e = hipMemcpyAsync(g_pinned_count, wb.counts + cur, sizeof(int32_t), hipMemcpyDeviceToHost, stream);
+    e = hipMemcpyAsync(g_pinned_live, ctl_live(wb), sizeof(int32_t), hipMemcpyDeviceToHost, stream);
     if (e != hipSuccess) return e;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return e;
-    if (*g_pinned_count == 0) break;
+    if (*g_pinned_live == 0) break;
   }
   prof_begin(kProfWfResolve, stream);
-  hipLaunchKernelGGL(wf_resolve, dim3(grid_for(wb.npix)), dim3(kBlock), 0, stream, fr, wb, batch, accum);
+  unsigned gr = (unsigned)((wb.npix + kBlock - 1) / kBlock);
+  if (gr > 2048) gr = 2048;
+  hipLaunchKernelGGL(wf_resolve, dim3(gr), dim3(kBlock), 0, stream, fr, wb, batch, accum);
   prof_end(kProfWfResolve, stream);
   return hipGetLastError();
 }
@@ -433,8 +525,8 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
   int32_t batch = s_count;
   while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
   if (layout(npix, batch).total > ws_bytes) return hipErrorInvalidValue;
-  if (!g_pinned_count) {
-    hipError_t e = hipHostMalloc((void**)&g_pinned_count, sizeof(int32_t), hipHostMallocDefault);
+  if (!g_pinned_live) {
+    hipError_t e = hipHostMalloc((void**)&g_pinned_live, sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) return e;
   }
   for (int32_t b0 = 0; b0 < s_count; b0 += batch) {
@@ -443,18 +535,18 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     char* p = (char*)ws;
     WfBufs wb;
     size_t c = (size_t)L.capacity;
-    for (int k = 0; k < 2; ++k) {
-      wb.q[k].a = (float4*)(p + L.q + (size_t)(3 * k + 0) * sizeof(float4) * c);
-      wb.q[k].b = (float4*)(p + L.q + (size_t)(3 * k + 1) * sizeof(float4) * c);
-      wb.q[k].c = (float4*)(p + L.q + (size_t)(3 * k + 2) * sizeof(float4) * c);
-    }
+    wb.q.a = (float4*)(p + L.q);
+    wb.q.b = (float4*)(p + L.q + sizeof(float4) * c);
+    wb.q.c = (float4*)(p + L.q + 2 * sizeof(float4) * c);
     wb.hit = (float2*)(p + L.hit);
     wb.medq = (int32_t*)(p + L.medq);
     wb.staging = (float*)(p + L.staging);
-    wb.counts = (int32_t*)(p + L.counts);
+    wb.ctl = (int32_t*)(p + L.ctl);
     wb.capacity = L.capacity;
+    wb.medseg = L.medseg;
     wb.npix = npix;
     wb.total = npix * nb;
+    wb.shard_len = (wb.total + kShards - 1) / kShards;
     wb.s_begin = s_begin + b0;
     hipError_t e;
     if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wb, accum, nb, counters, stream);

@@ -20,10 +20,19 @@ for s in "$@"; do
     explore) step explore 600 python tools/gpu_explore.py ;;
     bench) step bench 600 python bench.py ;;
     benchmk) step benchmk 600 python bench.py --variant mk --no-cpu-baseline ;;
-    rocprof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 4 --no-cpu-baseline ;;
+    benchwf) step benchwf 600 python bench.py --variant wf --no-cpu-baseline ;;
+    rocprof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py ;;
+    rocprofwf) step rocprofwf 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o benchwf -- python bench.py --variant wf --no-cpu-baseline ;;
+    traffic) step trafficf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic -o fetch -- python bench.py --steps 4 --no-cpu-baseline && step trafficw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/traffic -o write -- python bench.py --steps 4 --no-cpu-baseline ;;
+    trafficwf) step trafficwff 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic -o wffetch -- python bench.py --variant wf --steps 4 --no-cpu-baseline && step trafficwfw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/traffic -o wfwrite -- python bench.py --variant wf --steps 4 --no-cpu-baseline ;;
     ab) step ab 900 bash tools/gpu_ab.sh ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc -o pass1 -- python tools/ab.py mk 32 1 && step pmc2 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o pass2 -- python tools/ab.py mk 32 1 && step pmc3 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o pass3 -- python tools/ab.py mk 32 1 ;;
+    pmcwf) for ps in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" \
+                 "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_LEVEL_VMEM SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LEVEL_WAVES SQ_INSTS_LDS" \
+                 "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum" "TCP_TCC_ATOMIC_WITH_RET_REQ_sum TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum"; do
+             n=$((${n:-0}+1)); step pmcwf$n 600 rocprofv3 --pmc $ps --output-format csv -d gpurun_out/pmcwf -o p$n -- python tools/ab.py wf 64 1 || exit 1
+           done ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s" ;;
   esac
