@@ -390,6 +390,178 @@ __device__ __forceinline__ bool traverse_v1(const DevScene& sc, pt_v3 o, pt_v3 d
   return any;
 }
 
+// v1 with the top of the stack kept in registers: the child that v1 would
+// push last and pop next (the near child if it is hit, else the far one) is
+// carried to the next iteration in (cur, curE) and never touches LDS. The
+// visiting order, the pop-time cull `E <= closest` and the closest-hit
+// updates are v1's, step for step, so the hit is identical.
+template <int STACK>
+__device__ __forceinline__ bool traverse_v3(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
+                                            Stack st, float& t_out, int32_t& ref_out) {
+  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  float closest = tmax;
+  int32_t best = 0;
+  bool any = false;
+  int sp = 0;
+  int32_t cur = 0;
+  float curE = 0.0f;
+  bool have = false;
+  if (!(sc.n_inner == 0 && sc.root_ref >= 0)) {
+    float E, X;
+    slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
+         tmin, E, X);
+    if (pt_minf(X, closest) >= E) {
+      cur = sc.root_ref;
+      curE = E;
+      have = true;
+    }
+  }
+  while (have) {
+    have = false;
+    if (curE <= closest) {
+      if (cur < 0) {
+        float t;
+        if (hit_leaf(sc, cur, o, d, tmin, closest, t) && t < closest) {
+          closest = t;
+          best = cur;
+          any = true;
+        }
+      } else {
+        const float4* nd = sc.nodes + 4 * cur;
+        float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+        int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+        float E0, X0, E1, X1;
+        slab(o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
+        slab(o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
+        pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
+        pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
+        const bool ln = pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d);
+        const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
+        const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
+        const bool fh = ln ? (X1 >= E1) : (X0 >= E0), nh = ln ? (X0 >= E0) : (X1 >= E1);
+        if (nh) {  // v1: push far, push near, pop near
+          if (fh && sp < STACK) {
+            st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+            ++sp;
+          }
+          if (sp < STACK) {  // v1 drops the near child when the stack is full
+            cur = nr;
+            curE = nE;
+            have = true;
+          }
+        } else if (fh && sp < STACK) {  // v1: push far, pop far
+          cur = fr;
+          curE = fE;
+          have = true;
+        }
+      }
+    }
+    if (!have && sp > 0) {
+      --sp;
+      const uint2 ent = st.slot0[sp * kBlock];
+      cur = (int32_t)ent.x;
+      curE = __uint_as_float(ent.y);
+      have = true;
+    }
+  }
+  t_out = closest;
+  ref_out = best;
+  return any;
+}
+
+// v3 restructured as a while-while loop (inner nodes, then one leaf): a
+// lane that reaches a leaf waits until the other lanes of its wave have
+// reached theirs, so the wave runs node steps and leaf tests in lock-step
+// instead of every iteration paying both. Each lane's sequence of visits is
+// v3's unchanged (no speculation), so the hit is identical.
+template <int STACK>
+__device__ __forceinline__ bool traverse_v4(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
+                                            Stack st, float& t_out, int32_t& ref_out) {
+  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  const float4* __restrict__ nodes = sc.nodes;
+  float closest = tmax;
+  int32_t best = 0;
+  bool any = false;
+  int sp = 0;
+  int32_t cur = 0;
+  float curE = 0.0f;
+  bool have = false;
+  if (!(sc.n_inner == 0 && sc.root_ref >= 0)) {
+    float E, X;
+    slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
+         tmin, E, X);
+    if (pt_minf(X, closest) >= E) {
+      cur = sc.root_ref;
+      curE = E;
+      have = true;
+    }
+  }
+  while (have) {
+    while (have && cur >= 0) {  // inner nodes
+      have = false;
+      if (curE <= closest) {
+        const float4* nd = nodes + 4 * cur;
+        float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+        int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+        float E0, X0, E1, X1;
+        slab(o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
+        slab(o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
+        pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
+        pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
+        const bool ln = pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d);
+        const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
+        const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
+        const bool fh = ln ? (X1 >= E1) : (X0 >= E0), nh = ln ? (X0 >= E0) : (X1 >= E1);
+        if (nh) {
+          if (fh && sp < STACK) {
+            st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+            ++sp;
+          }
+          if (sp < STACK) {
+            cur = nr;
+            curE = nE;
+            have = true;
+          }
+        } else if (fh && sp < STACK) {
+          cur = fr;
+          curE = fE;
+          have = true;
+        }
+      }
+      if (!have && sp > 0) {
+        --sp;
+        const uint2 ent = st.slot0[sp * kBlock];
+        cur = (int32_t)ent.x;
+        curE = __uint_as_float(ent.y);
+        have = true;
+      }
+    }
+    if (have) {  // one leaf
+      if (curE <= closest) {
+        float t;
+        if (hit_leaf(sc, cur, o, d, tmin, closest, t) && t < closest) {
+          closest = t;
+          best = cur;
+          any = true;
+        }
+      }
+      have = false;
+      if (sp > 0) {
+        --sp;
+        const uint2 ent = st.slot0[sp * kBlock];
+        cur = (int32_t)ent.x;
+        curE = __uint_as_float(ent.y);
+        have = true;
+      }
+    }
+  }
+  t_out = closest;
+  ref_out = best;
+  return any;
+}
+
 #ifndef PTMI_TRAVERSAL
 #define PTMI_TRAVERSAL 1  // A/B on MI355X: push-both (1) beat the near-child shortcut (2) by 17%
 #endif
@@ -398,6 +570,10 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
                                          float& t_out, int32_t& ref_out) {
 #if PTMI_TRAVERSAL == 1
   return traverse_v1<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
+#elif PTMI_TRAVERSAL == 3
+  return traverse_v3<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
+#elif PTMI_TRAVERSAL == 4
+  return traverse_v4<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
 #else
   return traverse_v2<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
 #endif
@@ -420,6 +596,9 @@ __device__ __forceinline__ uint32_t mat_flags(const DevScene& sc, int32_t g) {
   return __float_as_uint(sc.mats[5 * g + 4].w);
 }
 
+#ifndef PTMI_PERLIN_UNROLL
+#define PTMI_PERLIN_UNROLL 1
+#endif
 __device__ __forceinline__ float perlin_noise(const DevScene& sc, pt_v3 p) {  // kernels.py:110-151
   float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
   float u = p.x - fx, v = p.y - fy, w = p.z - fz;
@@ -431,7 +610,8 @@ __device__ __forceinline__ float perlin_noise(const DevScene& sc, pt_v3 p) {  //
   const int32_t* py = sc.perlin_perm + 256;
   const int32_t* pz = sc.perlin_perm + 512;
   float accum = 0.0f;
-#pragma unroll
+  // outer corner loop rolled by default (-8 VGPRs; +2 % wavefront on MI355X)
+#pragma unroll PTMI_PERLIN_UNROLL
   for (int di = 0; di < 2; ++di)
 #pragma unroll
     for (int dj = 0; dj < 2; ++dj)

@@ -1,12 +1,21 @@
 #!/bin/bash
-# A/B all variant builds + default; each under its own timeout.
+# A/B all variant builds + default, two interleaved rounds; each run under its
+# own timeout. AB_PARITY=1 also runs the GPU parity tests against each variant.
 set -u
 shopt -s nullglob
 mkdir -p gpurun_out
-for v in ${AB_MODES:-mk wf}; do
-  timeout -k 10 120 python tools/ab.py $v 64 3 >> gpurun_out/ab.log 2>&1 || { echo "default $v failed rc=$?"; exit 1; }
-  for lib in path-tracer-python_amd/ptmi/_lib/variants/*.so; do
-    PTMI_LIB=$PWD/$lib timeout -k 10 120 python tools/ab.py $v 64 3 >> gpurun_out/ab.log 2>&1 || { echo "$lib $v failed rc=$?"; exit 1; }
+libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so path-tracer-python_amd/ptmi/_lib/variants/*.so)
+if [ "${AB_PARITY:-0}" = 1 ]; then
+  for lib in "${libs[@]}"; do
+    PTMI_LIB=$PWD/$lib timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x >> gpurun_out/ab_parity.log 2>&1
+    rc=$?; echo "parity $(basename $lib) rc=$rc"; [ $rc -le 1 ] || exit $rc
+  done
+fi
+for round in 1 2; do
+  for v in ${AB_MODES:-mk wf}; do
+    for lib in "${libs[@]}"; do
+      PTMI_LIB=$PWD/$lib timeout -k 10 120 python tools/ab.py $v 64 ${AB_REPS:-4} >> gpurun_out/ab.log 2>&1 || { echo "$lib $v failed rc=$?"; exit 1; }
+    done
   done
 done
 cp gpurun_out/ab.log /tmp/ab_copy.log; grep -h Msamples /tmp/ab_copy.log
