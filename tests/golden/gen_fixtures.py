@@ -217,6 +217,41 @@ def _sah_cases(sah):
     return out
 
 
+def crosscheck_ptmi(scenes_mod, scene_compiler, bvh_compiler, plan, seed):
+    """Drop-in check of the boundary: worlds built by the reference's own
+    scenes.py / core classes go through ptmi.scene_compiler.compile_scene and
+    ptmi.bvh.compile_bvh (native SAH builder), and every array must equal the
+    reference's compile_scene / compile_bvh output on the same world object.
+    Writes tests/golden/ptmi_crosscheck.json (data only)."""
+    sys.path.insert(0, os.path.join(OUT, '..', '..', 'path-tracer-python_amd'))
+    from ptmi import scene_compiler as pc, bvh as pb
+    result = {}
+    for name, (fn, _) in plan.items():
+        world, _cam = _capture(scenes_mod, fn, seed)
+        ref = scene_compiler.compile_scene(world)
+        ours = pc.compile_scene(world)
+        bad = []
+        for i in (0, 1, 3, 4, 6, 7):
+            for k, x in ref[i].items():
+                y = ours[i][k]
+                if isinstance(x, np.ndarray) and not (x.dtype == y.dtype and np.array_equal(x, y)):
+                    bad.append(f'{i}:{k}')
+                elif not isinstance(x, np.ndarray) and x != y:
+                    bad.append(f'{i}:{k}')
+        same_prims = all(a is b for i in (2, 5, 8) for a, b in zip(ref[i], ours[i])) and \
+            all(len(ref[i]) == len(ours[i]) for i in (2, 5, 8))
+        rb = bvh_compiler.compile_bvh(world, ref[2], ref[5], ref[8])
+        ob = pb.compile_bvh(world, ours[2], ours[5], ours[8])
+        for k, x in rb.items():
+            if isinstance(x, np.ndarray) and not np.array_equal(x, np.asarray(ob[k])):
+                bad.append(f'bvh:{k}')
+        result[name] = {'arrays_equal': not bad, 'mismatches': bad, 'same_primitive_objects': same_prims,
+                        'images': len(ours[10])}
+        print(name, result[name])
+    with open(os.path.join(OUT, 'ptmi_crosscheck.json'), 'w') as f:
+        json.dump({'numpy': np.__version__, 'seed': seed, 'scenes': result}, f, indent=1, sort_keys=True)
+
+
 def main():
     _install_stubs()
     os.chdir(REF_SRC)  # image_texture("assets/images/earthmap.jpg") is cwd-relative
@@ -232,6 +267,9 @@ def main():
         'cornell_smoke': ('cornell_smoke', [(800, None), (1024, None)]),
         'vol2_final_scene_comparison': ('vol2_final_scene_comparison', [(3840, 16.0 / 9.0)]),
     }
+    if '--crosscheck-ptmi' in sys.argv:
+        crosscheck_ptmi(scenes, scene_compiler, bvh_compiler, plan, seed)
+        return
     manifest = {'numpy': np.__version__, 'seed': seed, 'scenes': {}}
     earth = None
     for name, (fn, widths) in plan.items():

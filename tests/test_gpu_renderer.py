@@ -56,3 +56,45 @@ def test_render_sample_and_clear_compat():
         r.render_sample(i)
     assert np.array_equal(r.accum.cpu().numpy(), a)
     assert np.isfinite(a).all() and a.sum() > 0
+
+
+def test_interactive_viewer_headless(tmp_path):
+    """InteractiveViewer.render_interactive (interactive_viewer.py:327-451):
+    progressive batches give the same accumulator as one render(), and an
+    orbit rotation + restart renders the rotated camera from sample 0."""
+    from ptmi import scenes
+    from ptmi.interactive_viewer import InteractiveViewer
+    from ptmi.renderer import TaichiRenderer
+
+    def build(width=96, spp=7):
+        random.seed(1234)
+        sc = scenes.cornell_smoke()
+        sc.cam.img_width = width
+        sc.cam.samples_per_pixel = spp
+        return sc
+
+    sc = build()
+    v = InteractiveViewer(sc.world, sc.cam, str(tmp_path / 'v.png'))
+    v.background_color = sc.background
+    v.render_interactive()
+    assert v.current_sample == 7 and os.path.exists(tmp_path / 'v.png')
+    sc2 = build()
+    r = TaichiRenderer(sc2.world, sc2.cam, str(tmp_path / 'r.png'))
+    r.background_color = sc2.background
+    r.render(enable_preview=False)
+    assert np.array_equal(v.accum.cpu().numpy(), r.accum.cpu().numpy())
+
+    class Ev:
+        def __init__(self, x, y):
+            self.x, self.y = x, y
+    v.on_mouse_down(Ev(10, 10))
+    v.on_mouse_drag(Ev(40, 25))  # rotate (30, 15) px -> restart
+    assert v.current_sample == 0 and not v.accum.any()
+    v.render_interactive()
+    sc3 = build()
+    sc3.cam.lookfrom = v.cam.lookfrom
+    r3 = TaichiRenderer(sc3.world, sc3.cam, str(tmp_path / 'r3.png'))
+    r3.background_color = sc3.background
+    r3.render(enable_preview=False)
+    assert np.array_equal(v.accum.cpu().numpy(), r3.accum.cpu().numpy())
+    assert not np.array_equal(r3.accum.cpu().numpy(), r.accum.cpu().numpy())
