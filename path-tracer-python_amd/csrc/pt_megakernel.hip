@@ -60,9 +60,7 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
                                                            int32_t s_begin, int32_t s_count,
                                                            unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
-  __shared__ unsigned long long blk_cnt[3];
   const int tid = threadIdx.x;
-  if (tid < 3) blk_cnt[tid] = 0ull;
   Stack st{lds_stack + tid};
 
   // 16x16 pixel block = 4 waves of 8x8 (square footprints keep a wave's
@@ -185,12 +183,16 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
     ap[1] = acc.y;
     ap[2] = acc.z;
   }
-  if (counters) {
-    atomicAdd(&blk_cnt[0], n_seg);
-    atomicAdd(&blk_cnt[1], n_med);
-    atomicAdd(&blk_cnt[2], n_paths);
+  if (counters) {  // block sums in the (now idle) stack LDS: no extra LDS, 5 blocks/CU fit
     __syncthreads();
-    if (tid < 3) atomicAdd(counters + tid, blk_cnt[tid]);
+    unsigned long long* red = reinterpret_cast<unsigned long long*>(lds_stack);
+    if (tid < 3) red[tid] = 0ull;
+    __syncthreads();
+    atomicAdd(&red[0], n_seg);
+    atomicAdd(&red[1], n_med);
+    atomicAdd(&red[2], n_paths);
+    __syncthreads();
+    if (tid < 3) atomicAdd(counters + tid, red[tid]);
   }
 }
 

@@ -100,9 +100,15 @@ __device__ __forceinline__ void wave_add(bool flag, int32_t* counter, int32_t si
 }
 
 // Statistics counters: each thread tallies in a register over its grid-stride
-// loop; at kernel end the block sums through LDS and adds once.
-__device__ __forceinline__ void block_flush(uint32_t v, unsigned int* lds, unsigned long long* counter) {
+// loop; at kernel end the block sums through LDS and adds once. `scratch` may
+// alias LDS the kernel used before (the traversal stack): no extra LDS, which
+// would push a 32 KiB-stack block past 160 KiB / 5 and cost a wave per SIMD.
+__device__ __forceinline__ void block_flush(uint32_t v, void* scratch, unsigned long long* counter) {
+  unsigned int* lds = static_cast<unsigned int*>(scratch);
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if (threadIdx.x == 0) *lds = 0u;
+  __syncthreads();
   if (lane_id() == 0 && v) atomicAdd(lds, v);
   __syncthreads();
   if (threadIdx.x == 0 && *lds) atomicAdd(counter, (unsigned long long)*lds);
@@ -205,12 +211,9 @@ template <int STACK>
 __global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb,
                                                        unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
-  __shared__ unsigned int tally;
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
-  if (tid == 0) tally = 0;
   if (blockIdx.x < kShards && tid == 0) *ctl_medium(wb, blockIdx.x) = 0;  // medium counts of this iteration
-  __syncthreads();
   const Queue q = wb.q;
   uint32_t n_live = 0;
   for (int32_t i = (int32_t)(blockIdx.x * kBlock + tid); i < wb.capacity; i += (int32_t)(gridDim.x * kBlock)) {
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb,
     bool hit = traverse<STACK>(sc, o, d, kTMin, kTMax, st, t, ref);
     wb.hit[i] = make_float2(t, __int_as_float(hit ? ref : kMissRef));
   }
-  if (counters) block_flush(n_live, &tally, counters + 0);
+  if (counters) block_flush(n_live, lds_stack, counters + 0);
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
@@ -283,8 +286,6 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfB
   const int32_t stride = (int32_t)(gridDim.x * kBlock);
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
   __shared__ unsigned int tally;
-  if (threadIdx.x == 0) tally = 0;
-  __syncthreads();
   uint32_t n_ended = 0;
   for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < wb.capacity; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
@@ -335,20 +336,14 @@ template <int STACK>
 __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
                                                     unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
-  __shared__ int32_t seg_start[kShards + 1];
-  __shared__ unsigned int tally;
   Stack st{lds_stack + threadIdx.x};
-  if (threadIdx.x == 0) {
-    tally = 0;
-    int32_t acc = 0;
-    for (int s = 0; s < kShards; ++s) {
-      seg_start[s] = acc;
-      acc += *ctl_medium(wb, s);
-    }
-    seg_start[kShards] = acc;
+  int32_t cnt[kShards];  // per-shard medium counts (wave-uniform)
+  int32_t n = 0;
+#pragma unroll
+  for (int s = 0; s < kShards; ++s) {
+    cnt[s] = __builtin_amdgcn_readfirstlane(*ctl_medium(wb, s));
+    n += cnt[s];
   }
-  __syncthreads();
-  const int32_t n = seg_start[kShards];
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
   const int32_t stride = (int32_t)(gridDim.x * kBlock);
   uint32_t n_ended = 0;
@@ -358,8 +353,15 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
     Ray cont;
     int32_t i = -1, shard = 0;
     if (j < n) {
-      while (shard + 1 < kShards && j >= seg_start[shard + 1]) ++shard;
-      i = wb.medq[shard * wb.medseg + (j - seg_start[shard])];
+      int32_t off = j;
+#pragma unroll
+      for (int s = 0; s + 1 < kShards; ++s) {
+        if (shard == s && off >= cnt[s]) {
+          off -= cnt[s];
+          shard = s + 1;
+        }
+      }
+      i = wb.medq[shard * wb.medseg + off];
       const float2 h = wb.hit[i];
       const int32_t ref = __float_as_int(h.y);
       const Ray ray = load_ray(wb.q, i);
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
     finish_lane(fr, wb, i, (int32_t)(blockIdx.x % kShards), ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
-  if (counters) block_flush(n_ended, &tally, counters + 2);
+  if (counters) block_flush(n_ended, lds_stack, counters + 2);
 }
 
 // accum[pixel] += staging[s][p] for s = 0..batch-1 in order (render_sample's
