@@ -38,7 +38,15 @@ sys.path.insert(0, os.path.join(ROOT, 'path-tracer-python_amd'))
 
 METRIC = 'Msamples/s + achieved HBM GB/s, vol2_final_scene 800x800 at 1/2/4/8 MI355X'
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-BG = {'vol2_final_scene': (0.0, 0.0, 0.0), 'wavefront_comparison': (0.7, 0.8, 1.0), 'cornell_smoke': (0.0, 0.0, 0.0)}
+BG = {'vol2_final_scene': (0.0, 0.0, 0.0), 'vol2_final_scene_comparison': (0.0, 0.0, 0.0),
+      'wavefront_comparison': (0.7, 0.8, 1.0), 'cornell_smoke': (0.0, 0.0, 0.0)}
+# BASELINE.json configs as bench presets: (scene, width, integrator, spp per step, steps)
+PRESETS = {
+    'c2': ('vol2_final_scene', 800, 'mk', 64, 16),       # configs[1]; 16 steps = the 1024-spp north star
+    'c3': ('vol2_final_scene', 800, 'wf', 64, 16),       # configs[2]: wavefront, 1024 spp
+    'c4': ('cornell_mesh_fog', 1024, 'mk', 32, 16),      # configs[3]: OBJ mesh + fog, 512 spp
+    'c5': ('vol2_final_scene_comparison', 3840, 'mk', 16, 32),  # configs[4]: 4K, 512 spp per GPU (4096 on 8)
+}
 
 # Algorithmic HBM bytes per unit (DESIGN.md "Roofline"): what each kernel must
 # move at minimum for one unit of work in the queue layout of pt_wavefront.hip.
@@ -63,12 +71,14 @@ ALGO_BYTES = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
-    p.add_argument('--steps', type=int, default=16)
+    p.add_argument('--preset', choices=sorted(PRESETS), default='c2',
+                   help='BASELINE config; --scene/--width/--variant/--spp-per-step/--steps override it')
+    p.add_argument('--steps', type=int, default=None)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--spp-per-step', type=int, default=64)
-    p.add_argument('--variant', choices=('wf', 'mk'), default='mk')
-    p.add_argument('--scene', default='vol2_final_scene')
-    p.add_argument('--width', type=int, default=800)
+    p.add_argument('--spp-per-step', type=int, default=None)
+    p.add_argument('--variant', choices=('wf', 'mk'), default=None)
+    p.add_argument('--scene', default=None)
+    p.add_argument('--width', type=int, default=None)
     p.add_argument('--max-depth', type=int, default=50)
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -76,20 +86,51 @@ def parse():
     p.add_argument('--save-image', default='')
     p.add_argument('--shard', choices=('samples', 'tiles'), default='samples',
                    help='multi-GPU partition: disjoint sample shards (weak scaling) or row-band tiles (strong)')
-    return p.parse_args()
+    a = p.parse_args()
+    scene, width, variant, sps, steps = PRESETS[a.preset]
+    a.scene = a.scene or scene
+    a.width = a.width or width
+    a.variant = a.variant or variant
+    a.spp_per_step = a.spp_per_step or sps
+    a.steps = a.steps or steps
+    return a
 
 
-def cpu_baseline(scene, width, variant, max_depth, seed, budget_s):
+def load_workload(scene, width):
+    """(SceneArrays, camera upload dict, background, data note) of a workload:
+    the reference's own compiled arrays (tests/golden fixture) where captured,
+    else the scene built by ptmi.scenes at random.seed(1234) and compiled here
+    (compile_scene + native SAH builder)."""
+    from ptmi import scene_data as sd
+    import numpy as np
+    path = os.path.join(sd.golden_dir(), scene + '.npz')
+    if os.path.exists(path) and f'cam{width}_center' in np.load(path).files:
+        return (sd.load_fixture(scene), sd.fixture_camera(scene, width), BG[scene],
+                f'reference scene {scene} compiled at random.seed(1234) (tests/golden fixture); no external dataset')
+    import random
+    from ptmi import bvh as bvh_mod, core, scene_compiler, scenes
+    random.seed(1234)
+    sc = scenes.SCENES[scene]()
+    sc.cam.img_width = width
+    sc.cam.initialize()
+    perlin = core.perlin()
+    (geom, mats, spheres, qgeom, qmats, quads, tgeom, tmats, tris, _r, imgs) = scene_compiler.compile_scene(sc.world)
+    bvh = bvh_mod.compile_bvh(sc.world, spheres, quads, tris)
+    sa = sd.SceneArrays.from_compiled(geom, mats, qgeom, qmats, tgeom, tmats, bvh, perlin.tables(),
+                                      [scene_compiler.image_u8(t) for t in imgs])
+    return (sa, sd.camera_upload(sc.cam), tuple(sc.background),
+            f'{scene} built by ptmi.scenes at random.seed(1234) (build-supplied scene; OBJ asset in-tree); '
+            'no external dataset')
+
+
+def cpu_baseline(sa, cam, bg, scene, variant, max_depth, seed, budget_s):
     """Time the CPU oracle on a bounded slice of the workload (rank 0, N=1)."""
     import numpy as np
     import oracle
-    from ptmi import scene_data as sd
-    sa = sd.load_fixture(scene)
-    cam = sd.fixture_camera(scene, width)
     W, H = cam['width'], cam['height']
     threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
     osc = oracle.OracleScene(sa)
-    fr = oracle.make_frame(cam, BG[scene], max_depth, seed, W, H)
+    fr = oracle.make_frame(cam, bg, max_depth, seed, W, H)
     acc = np.zeros((H, W, 3), np.float32)
     rows = min(H, 64)
     y0 = (H - rows) // 2
@@ -143,12 +184,11 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     dev = torch.device('cuda', local_rank)
 
-    sa = sd.load_fixture(a.scene)
-    cam = sd.fixture_camera(a.scene, a.width)
+    sa, cam, bg, data_note = load_workload(a.scene, a.width)
     W, H = cam['width'], cam['height']
     integ = device.Integrator(device.DeviceScene(sd.pack_device(sa), dev))
     shard = Shard(rank, world, a.shard)
-    frame = device.make_frame(cam, BG[a.scene], a.max_depth, a.seed, W, H, band=shard.band())
+    frame = device.make_frame(cam, bg, a.max_depth, a.seed, W, H, band=shard.band())
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     render = integ.render_mk if a.variant == 'mk' else integ.render_wf
     sps = a.spp_per_step
@@ -212,8 +252,7 @@ def main():
         'scaling': 'weak' if a.shard == 'samples' else 'strong',
         'vs_baseline': None,
         'dtype': 'f32',
-        'data': 'reference scene vol2_final_scene compiled at random.seed(1234) (tests/golden fixture); '
-                'no external dataset',
+        'data': data_note,
         'config': {
             'workload': f'{a.scene} {W}x{H}, {"wavefront" if a.variant == "wf" else "megakernel"} integrator, '
                         f'{sps * a.steps} spp per GPU ({a.steps} steps x {sps} spp), max_depth {a.max_depth}',
@@ -239,7 +278,7 @@ def main():
         'pipeline_algorithmic_GBps': round(value * 1e6 * b_sample / 1e9, 3),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(a.scene, a.width, a.variant, a.max_depth, a.seed, a.cpu_seconds)
+        out['cpu_baseline'] = cpu_baseline(sa, cam, bg, a.scene, a.variant, a.max_depth, a.seed, a.cpu_seconds)
     elif rank == 0:
         out['cpu_baseline'] = None
     if rank == 0:

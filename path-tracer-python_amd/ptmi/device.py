@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .scene_data import DeviceLayout, SceneArrays, pack_device
+from .scene_data import DeviceLayout, SceneArrays, camera_upload, pack_device
 
 
 def _stream_ptr(stream=None):
@@ -85,14 +85,8 @@ def make_frame(cam, bg, max_depth, seed, width, height, window=None, band=(1, 1,
     """ptmi_frame from camera upload values (dict of f32 3-vectors or an
     object with the reference camera's attributes)."""
     f = _lib.Frame()
-    get = (lambda k: cam[k]) if isinstance(cam, dict) else None
-    if get is None:
-        def vec(p):
-            return np.array([p.x, p.y, p.z], np.float64).astype(np.float32)
-        vals = {'center': vec(cam.center), 'pixel00': vec(cam.pixel00_loc), 'delta_u': vec(cam.delta_u),
-                'delta_v': vec(cam.delta_v), 'defocus_u': vec(cam.defocus_disk_u),
-                'defocus_v': vec(cam.defocus_disk_v), 'defocus_angle': float(cam.defocus_angle)}
-        get = vals.__getitem__
+    vals = cam if isinstance(cam, dict) else camera_upload(cam)
+    get = vals.__getitem__
     for k, fld in (('center', 'center'), ('pixel00', 'pixel00'), ('delta_u', 'delta_u'), ('delta_v', 'delta_v'),
                    ('defocus_u', 'defocus_u'), ('defocus_v', 'defocus_v')):
         arr = np.asarray(get(k), np.float32)

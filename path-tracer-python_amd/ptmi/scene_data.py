@@ -153,6 +153,17 @@ def fixture_camera(name, width):
     return cam
 
 
+def camera_upload(cam):
+    """f32 camera upload values (renderer.py:230-247) of an initialized camera
+    object (ptmi.core.camera or the reference's), in fixture_camera's format."""
+    def vec(p):
+        return np.array([p.x, p.y, p.z], np.float64).astype(np.float32)
+    return {'center': vec(cam.center), 'pixel00': vec(cam.pixel00_loc), 'delta_u': vec(cam.delta_u),
+            'delta_v': vec(cam.delta_v), 'defocus_u': vec(cam.defocus_disk_u),
+            'defocus_v': vec(cam.defocus_disk_v), 'defocus_angle': float(cam.defocus_angle),
+            'width': int(cam.img_width), 'height': int(cam.img_height)}
+
+
 def fixture_manifest():
     with open(os.path.join(golden_dir(), 'manifest.json')) as f:
         return json.load(f)

@@ -21,6 +21,9 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     benchmk) step benchmk 600 python bench.py --variant mk --no-cpu-baseline ;;
     benchwf) step benchwf 600 python bench.py --variant wf --no-cpu-baseline ;;
+    benchc3) step benchc3 600 python bench.py --preset c3 ;;
+    benchc4) step benchc4 600 python bench.py --preset c4 ;;
+    benchc5) step benchc5 900 python bench.py --preset c5 --no-cpu-baseline ;;
     rocprof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py ;;
     rocprofwf) step rocprofwf 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o benchwf -- python bench.py --variant wf --no-cpu-baseline ;;
     traffic) step trafficf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic -o fetch -- python bench.py --steps 4 --no-cpu-baseline && step trafficw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/traffic -o write -- python bench.py --steps 4 --no-cpu-baseline ;;
