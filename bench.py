@@ -108,16 +108,12 @@ def load_workload(scene, width):
         return (sd.load_fixture(scene), sd.fixture_camera(scene, width), BG[scene],
                 f'reference scene {scene} compiled at random.seed(1234) (tests/golden fixture); no external dataset')
     import random
-    from ptmi import bvh as bvh_mod, core, scene_compiler, scenes
+    from ptmi import scenes
     random.seed(1234)
     sc = scenes.SCENES[scene]()
     sc.cam.img_width = width
     sc.cam.initialize()
-    perlin = core.perlin()
-    (geom, mats, spheres, qgeom, qmats, quads, tgeom, tmats, tris, _r, imgs) = scene_compiler.compile_scene(sc.world)
-    bvh = bvh_mod.compile_bvh(sc.world, spheres, quads, tris)
-    sa = sd.SceneArrays.from_compiled(geom, mats, qgeom, qmats, tgeom, tmats, bvh, perlin.tables(),
-                                      [scene_compiler.image_u8(t) for t in imgs])
+    sa = sd.compile_world(sc.world)
     return (sa, sd.camera_upload(sc.cam), tuple(sc.background),
             f'{scene} built by ptmi.scenes at random.seed(1234) (build-supplied scene; OBJ asset in-tree); '
             'no external dataset')

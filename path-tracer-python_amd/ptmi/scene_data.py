@@ -316,3 +316,17 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
         raise ValueError('Perlin permutation out of range')
     return DeviceLayout(nodes, root_ref, root_min, root_max, max_leaf_depth, spheres, quads, tris, mats,
                         texels, offs, ws, hs, pv, perm, ns, nq, nt)
+
+
+def compile_world(world, perlin_tables=None):
+    """World -> SceneArrays the way the renderer does it (renderer.py:65-100):
+    Perlin tables from a perlin() created after the scene (it draws from the
+    global `random` stream), compile_scene, native SAH BVH, RGB8 images."""
+    from . import bvh as bvh_mod, core, scene_compiler
+    if perlin_tables is None:
+        perlin_tables = core.perlin().tables()
+    (geom, mats, spheres, qgeom, qmats, quads, tgeom, tmats, tris, _reg,
+     img_list) = scene_compiler.compile_scene(world)
+    bvh = bvh_mod.compile_bvh(world, spheres, quads, tris)
+    return SceneArrays.from_compiled(geom, mats, qgeom, qmats, tgeom, tmats, bvh, perlin_tables,
+                                     [scene_compiler.image_u8(t) for t in img_list])

@@ -23,6 +23,9 @@ CASES = [
     ('vol2_final_scene', 800, (560, 200, 48, 48), 4),            # earth / noise spheres region
     ('cornell_smoke', 800, (300, 300, 64, 64), 4),               # smoke volumes (quad media)
     ('vol2_final_scene', 64, (0, 0, 64, 64), 8),                 # small full frame
+    ('coverage', 160, (0, 0, 160, 90), 8),                       # checker/image-on-quad/triangles/defocus
+    ('cornell_mesh_fog', 1024, (448, 448, 64, 64), 4),           # BASELINE configs[3]: OBJ torus + fog
+    ('cornell_mesh_fog', 96, (0, 0, 96, 96), 4),                 # same scene, small full frame
 ]
 
 

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity_helpers import BG, fixture, oracle_render
+from parity_helpers import BG, fixture, oracle_render, scene_inputs
 from ptmi import scene_data as sd
 
 
@@ -48,22 +48,49 @@ def brute_force(sa, o, d, tmin=np.float32(0.001), tmax=np.float32(1e10)):
                 be = dot(w, cross(q['quad_u'][i], p))
                 if 0 <= al <= 1 and 0 <= be <= 1 and t < best_t:
                     best_t, best = t, (2, i)
+    tr = sa.tris
+    if sa.num_triangles:  # kernels.py:252-307, vectorised over triangles (elementwise f32, same op order)
+        v0, e1, e2 = tr['triangle_v0'], tr['triangle_edge1'], tr['triangle_edge2']
+        f = np.float32
+
+        def vdot(a, b):
+            return (a[:, 0] * b[:, 0] + a[:, 1] * b[:, 1]) + a[:, 2] * b[:, 2]
+
+        def vcross(a, b):
+            return np.stack([a[:, 1] * b[:, 2] - a[:, 2] * b[:, 1], a[:, 2] * b[:, 0] - a[:, 0] * b[:, 2],
+                             a[:, 0] * b[:, 1] - a[:, 1] * b[:, 0]], axis=1)
+        dd = np.broadcast_to(d, e2.shape).astype(f)
+        hv = vcross(dd, e2)
+        det = vdot(e1, hv)
+        ok = np.abs(det) >= f(1e-8)
+        with np.errstate(divide='ignore', invalid='ignore', over='ignore'):
+            inv = f(1.0) / det
+            sv = (o - v0).astype(f)
+            u = inv * vdot(sv, hv)
+            q = vcross(sv, e1)
+            v = inv * vdot(dd, q)
+            t = inv * vdot(e2, q)
+        ok &= (u >= 0) & (u <= 1) & (v >= 0) & (u + v <= 1) & (t >= tmin) & (t <= tmax)
+        for i in np.nonzero(ok)[0]:  # in index order: first-found on equal t, like the scan above
+            if t[i] < best_t:
+                best_t, best = t[i], (1, int(i))
     return best_t, best
 
 
-@pytest.mark.parametrize('name', ['wavefront_comparison', 'cornell_smoke'])
+@pytest.mark.parametrize('name', ['wavefront_comparison', 'cornell_smoke', 'coverage'])
 def test_traversal_matches_brute_force(name):
-    sa = fixture(name)
+    sa, cam, _ = scene_inputs(name, 800 if name != 'coverage' else 160)
     osc = oracle.OracleScene(sa)
     rng = np.random.default_rng(5)
-    cam = sd.fixture_camera(name, 800)
     agree = 0
     n = 300
+    tri_hits = 0
     for _ in range(n):
         o = cam['center'] + rng.normal(0, 0.5, 3).astype(np.float32)
-        d = (cam['pixel00'] + rng.uniform(0, 800) * cam['delta_u'] + rng.uniform(0, cam['height']) * cam['delta_v']
+        d = (cam['pixel00'] + rng.uniform(0, cam['width']) * cam['delta_u'] + rng.uniform(0, cam['height']) * cam['delta_v']
              - o).astype(np.float32)
         hit, t, ty, ix = oracle.traverse(osc, o, d)
+        tri_hits += bool(hit and ty == 1)
         bt, (bty, bix) = brute_force(sa, o.astype(np.float32), d)
         if bty < 0:
             assert not hit
@@ -73,6 +100,8 @@ def test_traversal_matches_brute_force(name):
             assert t == bt
             agree += (ty, ix) == (bty, bix)
     assert agree >= n - 2  # exact float ties may resolve differently
+    if sa.num_triangles:
+        assert tri_hits >= 5
 
 
 @pytest.fixture(scope='module')
