@@ -36,8 +36,10 @@ enum {
  * replaces the field uploads of renderer.py:102-228 / fields.py:25-153).
  * Layouts (all little-endian, 16-byte aligned):
  *   nodes   : n_inner x 16 f32 — internal BVH2 node holding BOTH children's
- *             boxes: {c0.min.xyz, c0.max.x | c0.max.yz, c1.min.xy |
- *             c1.min.z, c1.max.xyz | ref0, ref1, 0, 0 (as i32 bits)}.
+ *             boxes, interleaved per component so the two children form
+ *             packed-f32 pairs: {min.x c0,c1, min.y c0,c1 | min.z c0,c1,
+ *             max.x c0,c1 | max.y c0,c1, max.z c0,c1 | ref0, ref1, 0, 0
+ *             (as i32 bits)}.
  *             ref >= 0: internal node index; ref < 0: leaf code
  *             0x80000000 | type << 28 | prim index (type: 0 sphere,
  *             1 triangle, 2 quad — scene_compiler.py:10-12).

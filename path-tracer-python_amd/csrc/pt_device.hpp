@@ -225,10 +225,23 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // t < closest_t. Each stack entry carries the child's slab entry distance E
 // (computed once when the parent is expanded); the reference's pop-time
 // test max(E, t_min) <= min(X, closest_t) is split exactly into X >= E (at
-// push) and E <= closest_t (at pop). The near child is not pushed and popped
-// again: it is taken directly (same test, same closest_t), so only far
-// children touch the stack. Stack: STACK 8-byte {ref, E} slots per thread in
-// LDS, slot-major, so a wave's ds_read_b64/ds_write_b64 hit distinct banks.
+// push) and E <= closest_t (at pop). Stack: STACK 8-byte {ref, E} slots per
+// thread in LDS, slot-major, so a wave's ds_read_b64/ds_write_b64 hit
+// distinct banks.
+//
+// Node layout (include/ptmi.h): the two children's box coordinates are
+// interleaved per component — {lo.x L,R | lo.y L,R}{lo.z L,R | hi.x L,R}
+// {hi.y L,R | hi.z L,R}{ref L, ref R, -, -} — so both children's slabs and
+// centre distances run as packed-f32 pairs (v_pk_add/v_pk_mul: one
+// instruction per component for both children). Packed ops are IEEE f32 per
+// half, so every value is bit-identical to the scalar restatement.
+//
+// A/B history on MI355X (all parity-identical): near-child shortcut with a
+// nested pop loop -17 %; top of stack in registers +0-2 % (mk) / -3 % (wf);
+// while-while -15 %; persistent lanes refilled per ray (wf) -7 %. This
+// push-both loop is the fastest measured.
+
+typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
 struct Stack {
   uint2* slot0;  // &lds[tid]; slot k at slot0[k * kBlock]
@@ -243,110 +256,41 @@ __device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, f
   X = pt_minf(pt_minf(pt_maxf(t0x, t1x), pt_maxf(t0y, t1y)), pt_maxf(t0z, t1z));
 }
 
+__device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
+
+#ifndef PTMI_NODES_VGPR
+#define PTMI_NODES_VGPR 1  // A/B on MI355X: +2 % megakernel
+#endif
+
 template <int STACK>
-__device__ __forceinline__ bool traverse_v2(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
-                                            Stack st, float& t_out, int32_t& ref_out) {
-  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
-                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
+                                         float& t_out, int32_t& ref_out) {
+  const pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                           fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  typedef const __attribute__((address_space(1))) float4 gfloat4;  // global: global_load, not flat_load
+  gfloat4* nodes = (gfloat4*)sc.nodes;
+#if PTMI_NODES_VGPR
+  // keep the node base in VGPRs: under SGPR pressure the compiler otherwise
+  // re-loads it from the kernarg segment on every visit (s_load + lgkmcnt wait
+  // on the pop's critical path)
+  asm volatile("" : "+v"(nodes));
+#endif
+  const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
+  const pt_f2 ix = pt_f2s(inv.x), iy = pt_f2s(inv.y), iz = pt_f2s(inv.z);
+  const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
   float closest = tmax;
   int32_t best = 0;
   bool any = false;
+  int sp = 0;
   if (sc.n_inner == 0 && sc.root_ref >= 0) {  // empty scene
     t_out = tmax;
     ref_out = 0;
     return false;
   }
-  int sp = 0;
-  int32_t cur = sc.root_ref;
-  bool have;
   {
     float E, X;
     slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
          tmin, E, X);
-    have = pt_minf(X, closest) >= E;
-  }
-  while (have) {
-    if (cur < 0) {  // leaf: kernels.py:671-697
-      float t;
-      if (hit_leaf(sc, cur, o, d, tmin, closest, t) && t < closest) {
-        closest = t;
-        best = cur;
-        any = true;
-      }
-    } else {  // internal: kernels.py:698-740
-      const float4* nd = sc.nodes + 4 * cur;
-      const float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-      float E0, X0, E1, X1;
-      slab(o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
-      slab(o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
-      pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
-      pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
-      const bool left_near = pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d);
-      const int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-      const int32_t nr = left_near ? r0 : r1, fr = left_near ? r1 : r0;
-      const float nE = left_near ? E0 : E1, fE = left_near ? E1 : E0;
-      const bool nh = left_near ? (X0 >= E0) : (X1 >= E1);
-      const bool fh = left_near ? (X1 >= E1) : (X0 >= E0);
-      if (nh && nE <= closest) {
-        if (fh && sp < STACK) {
-          st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
-          ++sp;
-        }
-        cur = nr;
-        continue;
-      }
-      if (fh && fE <= closest) {
-        cur = fr;
-        continue;
-      }
-    }
-    have = false;  // pop the next live entry
-    while (sp > 0) {
-      --sp;
-      const uint2 ent = st.slot0[sp * kBlock];
-      if (__uint_as_float(ent.y) <= closest) {
-        cur = (int32_t)ent.x;
-        have = true;
-        break;
-      }
-    }
-  }
-  t_out = closest;
-  ref_out = best;
-  return any;
-}
-
-// Variant without the near-child shortcut (every child pushed), kept for A/B
-// timing (PTMI_TRAVERSAL=1).
-
-__device__ __forceinline__ void child_slab_v1(float4 lo_a, pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz,
-                                           float mxx, float mxy, float mxz, float tmin, float& E, float& X) {
-  float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
-  float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
-  float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
-  E = pt_maxf(pt_maxf(pt_minf(t0x, t1x), pt_minf(t0y, t1y)), pt_maxf(pt_minf(t0z, t1z), tmin));
-  X = pt_minf(pt_minf(pt_maxf(t0x, t1x), pt_maxf(t0y, t1y)), pt_maxf(t0z, t1z));
-  (void)lo_a;
-}
-
-template <int STACK>
-__device__ __forceinline__ bool traverse_v1(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
-                                         Stack st, float& t_out, int32_t& ref_out) {
-  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
-                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
-  float closest = tmax;
-  int32_t best = 0;
-  bool any = false;
-  int sp = 0;
-  if (sc.n_inner == 0 && sc.root_ref >= 0) {  // empty scene
-    t_out = tmax;
-    ref_out = 0;
-    return false;
-  }
-  {
-    float E, X;
-    child_slab_v1(float4(), o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0],
-               sc.root_max[1], sc.root_max[2], tmin, E, X);
     if (pt_minf(X, closest) >= E) {
       st.slot0[0] = make_uint2((uint32_t)sc.root_ref, __float_as_uint(E));
       sp = 1;
@@ -355,10 +299,9 @@ __device__ __forceinline__ bool traverse_v1(const DevScene& sc, pt_v3 o, pt_v3 d
   while (sp > 0) {
     --sp;
     const uint2 ent = st.slot0[sp * kBlock];
-    int32_t ref = (int32_t)ent.x;
-    float te = __uint_as_float(ent.y);
-    if (!(te <= closest)) continue;
-    if (ref < 0) {
+    const int32_t ref = (int32_t)ent.x;
+    if (!(__uint_as_float(ent.y) <= closest)) continue;
+    if (ref < 0) {  // leaf: kernels.py:671-697
       float t;
       if (hit_leaf(sc, ref, o, d, tmin, closest, t) && t < closest) {
         closest = t;
@@ -367,216 +310,42 @@ __device__ __forceinline__ bool traverse_v1(const DevScene& sc, pt_v3 o, pt_v3 d
       }
       continue;
     }
-    const float4* nd = sc.nodes + 4 * ref;
-    float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-    int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-    float E0, X0, E1, X1;
-    child_slab_v1(a, o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
-    child_slab_v1(a, o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
-    pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
-    pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
-    float ld = pt_dot(pt_sub(lc, o), d);
-    float rd = pt_dot(pt_sub(rc, o), d);
-    bool h0 = X0 >= E0, h1 = X1 >= E1;
-    // push far first: left nearer -> push right then left
-    int32_t fr = (ld < rd) ? r1 : r0, nr = (ld < rd) ? r0 : r1;
-    float fE = (ld < rd) ? E1 : E0, nE = (ld < rd) ? E0 : E1;
-    bool fh = (ld < rd) ? h1 : h0, nh = (ld < rd) ? h0 : h1;
-    if (fh && sp < STACK) { st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE)); ++sp; }
-    if (nh && sp < STACK) { st.slot0[sp * kBlock] = make_uint2((uint32_t)nr, __float_as_uint(nE)); ++sp; }
-  }
-  t_out = closest;
-  ref_out = best;
-  return any;
-}
-
-// v1 with the top of the stack kept in registers: the child that v1 would
-// push last and pop next (the near child if it is hit, else the far one) is
-// carried to the next iteration in (cur, curE) and never touches LDS. The
-// visiting order, the pop-time cull `E <= closest` and the closest-hit
-// updates are v1's, step for step, so the hit is identical.
-template <int STACK>
-__device__ __forceinline__ bool traverse_v3(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
-                                            Stack st, float& t_out, int32_t& ref_out) {
-  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
-                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
-  float closest = tmax;
-  int32_t best = 0;
-  bool any = false;
-  int sp = 0;
-  int32_t cur = 0;
-  float curE = 0.0f;
-  bool have = false;
-  if (!(sc.n_inner == 0 && sc.root_ref >= 0)) {
-    float E, X;
-    slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
-         tmin, E, X);
-    if (pt_minf(X, closest) >= E) {
-      cur = sc.root_ref;
-      curE = E;
-      have = true;
+    // internal: kernels.py:698-740, both children at once
+    gfloat4* nd = nodes + 4 * ref;
+    const float4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
+    const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
+    const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
+    const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
+    const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
+    const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
+    const float E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)),
+                             pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
+    const float X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
+    const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)),
+                             pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
+    const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
+    // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
+    const pt_f2 half = pt_f2s(0.5f);
+    const pt_f2 dist = (((lox + hix) * half - ox) * dx + ((loy + hiy) * half - oy) * dy) +
+                       ((loz + hiz) * half - oz) * dz;
+    const bool ln = dist.x < dist.y;
+    const int32_t r0 = __float_as_int(R.x), r1 = __float_as_int(R.y);
+    const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
+    const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
+    const bool h0 = X0 >= E0, h1 = X1 >= E1;
+    const bool fh = ln ? h1 : h0, nh = ln ? h0 : h1;
+    if (fh && sp < STACK) {  // far first
+      st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+      ++sp;
     }
-  }
-  while (have) {
-    have = false;
-    if (curE <= closest) {
-      if (cur < 0) {
-        float t;
-        if (hit_leaf(sc, cur, o, d, tmin, closest, t) && t < closest) {
-          closest = t;
-          best = cur;
-          any = true;
-        }
-      } else {
-        const float4* nd = sc.nodes + 4 * cur;
-        float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-        int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-        float E0, X0, E1, X1;
-        slab(o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
-        slab(o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
-        pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
-        pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
-        const bool ln = pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d);
-        const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
-        const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
-        const bool fh = ln ? (X1 >= E1) : (X0 >= E0), nh = ln ? (X0 >= E0) : (X1 >= E1);
-        if (nh) {  // v1: push far, push near, pop near
-          if (fh && sp < STACK) {
-            st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
-            ++sp;
-          }
-          if (sp < STACK) {  // v1 drops the near child when the stack is full
-            cur = nr;
-            curE = nE;
-            have = true;
-          }
-        } else if (fh && sp < STACK) {  // v1: push far, pop far
-          cur = fr;
-          curE = fE;
-          have = true;
-        }
-      }
-    }
-    if (!have && sp > 0) {
-      --sp;
-      const uint2 ent = st.slot0[sp * kBlock];
-      cur = (int32_t)ent.x;
-      curE = __uint_as_float(ent.y);
-      have = true;
+    if (nh && sp < STACK) {
+      st.slot0[sp * kBlock] = make_uint2((uint32_t)nr, __float_as_uint(nE));
+      ++sp;
     }
   }
   t_out = closest;
   ref_out = best;
   return any;
-}
-
-// v3 restructured as a while-while loop (inner nodes, then one leaf): a
-// lane that reaches a leaf waits until the other lanes of its wave have
-// reached theirs, so the wave runs node steps and leaf tests in lock-step
-// instead of every iteration paying both. Each lane's sequence of visits is
-// v3's unchanged (no speculation), so the hit is identical.
-template <int STACK>
-__device__ __forceinline__ bool traverse_v4(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax,
-                                            Stack st, float& t_out, int32_t& ref_out) {
-  pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
-                     fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
-  const float4* __restrict__ nodes = sc.nodes;
-  float closest = tmax;
-  int32_t best = 0;
-  bool any = false;
-  int sp = 0;
-  int32_t cur = 0;
-  float curE = 0.0f;
-  bool have = false;
-  if (!(sc.n_inner == 0 && sc.root_ref >= 0)) {
-    float E, X;
-    slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
-         tmin, E, X);
-    if (pt_minf(X, closest) >= E) {
-      cur = sc.root_ref;
-      curE = E;
-      have = true;
-    }
-  }
-  while (have) {
-    while (have && cur >= 0) {  // inner nodes
-      have = false;
-      if (curE <= closest) {
-        const float4* nd = nodes + 4 * cur;
-        float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-        int32_t r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-        float E0, X0, E1, X1;
-        slab(o, inv, a.x, a.y, a.z, a.w, b.x, b.y, tmin, E0, X0);
-        slab(o, inv, b.z, b.w, c.x, c.y, c.z, c.w, tmin, E1, X1);
-        pt_v3 lc = pt_v3f((a.x + a.w) * 0.5f, (a.y + b.x) * 0.5f, (a.z + b.y) * 0.5f);
-        pt_v3 rc = pt_v3f((b.z + c.y) * 0.5f, (b.w + c.z) * 0.5f, (c.x + c.w) * 0.5f);
-        const bool ln = pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d);
-        const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
-        const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
-        const bool fh = ln ? (X1 >= E1) : (X0 >= E0), nh = ln ? (X0 >= E0) : (X1 >= E1);
-        if (nh) {
-          if (fh && sp < STACK) {
-            st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
-            ++sp;
-          }
-          if (sp < STACK) {
-            cur = nr;
-            curE = nE;
-            have = true;
-          }
-        } else if (fh && sp < STACK) {
-          cur = fr;
-          curE = fE;
-          have = true;
-        }
-      }
-      if (!have && sp > 0) {
-        --sp;
-        const uint2 ent = st.slot0[sp * kBlock];
-        cur = (int32_t)ent.x;
-        curE = __uint_as_float(ent.y);
-        have = true;
-      }
-    }
-    if (have) {  // one leaf
-      if (curE <= closest) {
-        float t;
-        if (hit_leaf(sc, cur, o, d, tmin, closest, t) && t < closest) {
-          closest = t;
-          best = cur;
-          any = true;
-        }
-      }
-      have = false;
-      if (sp > 0) {
-        --sp;
-        const uint2 ent = st.slot0[sp * kBlock];
-        cur = (int32_t)ent.x;
-        curE = __uint_as_float(ent.y);
-        have = true;
-      }
-    }
-  }
-  t_out = closest;
-  ref_out = best;
-  return any;
-}
-
-#ifndef PTMI_TRAVERSAL
-#define PTMI_TRAVERSAL 1  // A/B on MI355X: push-both (1) beat the near-child shortcut (2) by 17%
-#endif
-template <int STACK>
-__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
-                                         float& t_out, int32_t& ref_out) {
-#if PTMI_TRAVERSAL == 1
-  return traverse_v1<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
-#elif PTMI_TRAVERSAL == 3
-  return traverse_v3<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
-#elif PTMI_TRAVERSAL == 4
-  return traverse_v4<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
-#else
-  return traverse_v2<STACK>(sc, o, d, tmin, tmax, st, t_out, ref_out);
-#endif
 }
 
 // ---------------------------------------------------------------- textures

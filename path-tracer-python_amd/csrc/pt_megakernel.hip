@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
   } else {
     s = s_end;
   }
-  unsigned long long n_seg = 0, n_med = 0, n_paths = 0;
+  uint32_t n_seg = 0, n_med = 0, n_paths = 0;  // per-thread counts of one launch
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
   PathState ps;
   if (s < s_end) start_path(fr, px, py, s, ps);
@@ -188,9 +188,9 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
     unsigned long long* red = reinterpret_cast<unsigned long long*>(lds_stack);
     if (tid < 3) red[tid] = 0ull;
     __syncthreads();
-    atomicAdd(&red[0], n_seg);
-    atomicAdd(&red[1], n_med);
-    atomicAdd(&red[2], n_paths);
+    atomicAdd(&red[0], (unsigned long long)n_seg);
+    atomicAdd(&red[1], (unsigned long long)n_med);
+    atomicAdd(&red[2], (unsigned long long)n_paths);
     __syncthreads();
     if (tid < 3) atomicAdd(counters + tid, red[tid]);
   }

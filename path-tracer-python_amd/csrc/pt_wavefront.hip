@@ -215,8 +215,9 @@ __global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb,
   Stack st{lds_stack + tid};
   if (blockIdx.x < kShards && tid == 0) *ctl_medium(wb, blockIdx.x) = 0;  // medium counts of this iteration
   const Queue q = wb.q;
+  const int32_t stride = (int32_t)(gridDim.x * kBlock);
   uint32_t n_live = 0;
-  for (int32_t i = (int32_t)(blockIdx.x * kBlock + tid); i < wb.capacity; i += (int32_t)(gridDim.x * kBlock)) {
+  for (int32_t i = (int32_t)(blockIdx.x * kBlock + tid); i < wb.capacity; i += stride) {
     if (slot_item(q, i) == kDead) continue;
     ++n_live;
     float4 a = q.a[i], b = q.b[i];

@@ -264,12 +264,10 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
     codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | pidx.astype(np.int64)) - (1 << 32)).astype(np.int32)
     refs = np.where(is_leaf, codes, cidx.astype(np.int32)).astype(np.int32)
     nodes = np.zeros((internal.shape[0], 16), np.float32)
-    if internal.size:
+    if internal.size:  # children interleaved per component (include/ptmi.h)
         l, r = left[internal], right[internal]
-        nodes[:, 0:3] = bmin[l]
-        nodes[:, 3:6] = bmax[l]
-        nodes[:, 6:9] = bmin[r]
-        nodes[:, 9:12] = bmax[r]
+        nodes[:, 0:12:2] = np.concatenate([bmin[l], bmax[l]], axis=1)
+        nodes[:, 1:12:2] = np.concatenate([bmin[r], bmax[r]], axis=1)
         nodes[:, 12] = refs[l].view(np.float32)
         nodes[:, 13] = refs[r].view(np.float32)
     if n:
