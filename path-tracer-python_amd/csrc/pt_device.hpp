@@ -267,8 +267,11 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
                                          float& t_out, int32_t& ref_out) {
   const pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
                            fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
-  typedef const __attribute__((address_space(1))) float4 gfloat4;  // global: global_load, not flat_load
-  gfloat4* nodes = (gfloat4*)sc.nodes;
+  // global address space: global_load, not flat_load (a laundered generic
+  // pointer would otherwise lose it); clang vector type, no C++ copy ctor
+  typedef float pt_f4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) pt_f4 gf4;
+  gf4* nodes = (gf4*)sc.nodes;
 #if PTMI_NODES_VGPR
   // keep the node base in VGPRs: under SGPR pressure the compiler otherwise
   // re-loads it from the kernarg segment on every visit (s_load + lgkmcnt wait
@@ -311,8 +314,8 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
       continue;
     }
     // internal: kernels.py:698-740, both children at once
-    gfloat4* nd = nodes + 4 * ref;
-    const float4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
+    gf4* nd = nodes + 4 * ref;
+    const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
     const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
     const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
     const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
