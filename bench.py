@@ -65,6 +65,8 @@ ALGO_BYTES = {
     'wf_generate': ('rays', 48),
     # accumulator read + write 24 B + batch x 12 B staging read, per pixel
     'wf_resolve': ('pixels', 24),
+    # accumulator read + write 24 B + batch x 12 B staging read, per pixel
+    'mk_resolve': ('pixels', 24),
 }
 
 
@@ -84,6 +86,9 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--save-image', default='')
+    p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
+                   help='nccl = RCCL over xGMI (the product path); gloo only to rehearse the multi-rank flow '
+                        'with several ranks on one GPU (host-side reduce)')
     p.add_argument('--shard', choices=('samples', 'tiles'), default='samples',
                    help='multi-GPU partition: disjoint sample shards (weak scaling) or row-band tiles (strong)')
     a = p.parse_args()
@@ -174,11 +179,16 @@ def main():
     world = a.gpus
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    # one process per GPU; the gloo rehearsal may put several ranks on one device
+    dev_index = local_rank if a.dist_backend == 'nccl' else local_rank % max(1, torch.cuda.device_count())
+    dev = torch.device('cuda', dev_index)
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    dev = torch.device('cuda', local_rank)
+        torch.cuda.set_device(dev)
+        if a.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
     sa, cam, bg, data_note = load_workload(a.scene, a.width)
     W, H = cam['width'], cam['height']
@@ -213,7 +223,7 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dev)
+    elapsed = max_over_ranks(elapsed, dev if a.dist_backend == 'nccl' else None)
     cnt = integ.read_counters()
     rows_rank = len(shard.rows(H))
     samples_rank = W * rows_rank * sps * a.steps
@@ -230,7 +240,8 @@ def main():
         unit_bytes = b_sample
     units = {'wf_intersect': cnt['segments'], 'wf_shade': cnt['segments'], 'wf_medium': cnt['medium'],
              'megakernel': samples_rank,
-             'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches']}[dom]
+             'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
+             'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]
     dom_ms = prof[dom]['ms']
     launches = prof[dom]['launches']
     achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -254,7 +265,8 @@ def main():
                         f'{sps * a.steps} spp per GPU ({a.steps} steps x {sps} spp), max_depth {a.max_depth}',
             'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'spp_per_step': sps,
             'spp_per_gpu': sps * a.steps if a.shard == 'samples' else f'{sps * a.steps} (rows 1/{world})', 'max_depth': a.max_depth, 'seed': a.seed,
-            'parallelism': (f'{a.shard}-shard x{world} + RCCL reduce' if world > 1 else 'single GPU'),
+            'parallelism': (f'{a.shard}-shard x{world} + {"RCCL" if a.dist_backend == "nccl" else "gloo"} reduce'
+                            if world > 1 else 'single GPU'),
         },
         'roofline': {
             'bound': 'hbm', 'kernel': dom,

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 1
+#define PTMI_ABI_VERSION 2
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -115,6 +115,19 @@ int ptmi_scene_check(const ptmi_scene_view *scene);
 int ptmi_mk_render(const ptmi_scene_view *scene, const ptmi_frame *frame, float *accum,
                    int32_t sample_begin, int32_t sample_count, uint64_t *counters, void *stream);
 
+/* Megakernel over (16x16 tile, chunk of samples) work units — enough units
+ * to fill the chip for ~16 rounds, so a launch does not end in a long,
+ * partially occupied last round. Each path's colour goes to a staging slot
+ * [sample][pixel] of `workspace` and a resolve kernel adds them into accum in
+ * sample order: same results, bit for bit, as ptmi_mk_render. workspace:
+ * device memory (16-byte aligned) of at least ptmi_mk_workspace_bytes(frame, 1)
+ * bytes; ptmi_mk_workspace_bytes(frame, B) = 12 * pixels * B (rounded up)
+ * lets one batch hold B samples. Asynchronous, graph-capturable. */
+size_t ptmi_mk_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
+int ptmi_mk_render_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
+                      size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
+                      uint64_t *counters, void *stream);
+
 /* Wavefront: replaces generate_camera_rays / intersect_rays /
  * shade_miss_rays / reset_next_ray_count / shade_and_scatter /
  * swap_ray_buffers (kernels.py:1219-1418) as driven by
@@ -156,9 +169,9 @@ int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int
  * then record around every kernel; ptmi_prof_stop synchronises, returns the
  * summed milliseconds and launch counts per kernel kind
  * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 wf_shade, 4 wf_medium,
- * 5 wf_resolve} and disables timing. Not thread-safe; one profiling session
- * per process. */
-#define PTMI_PROF_KINDS 6
+ * 5 wf_resolve, 6 mk_resolve} and disables timing. Not thread-safe; one
+ * profiling session per process. */
+#define PTMI_PROF_KINDS 7
 int ptmi_prof_start(int32_t max_launches);
 int ptmi_prof_stop(double *ms_by_kernel, uint64_t *launches_by_kernel, int32_t n_kinds);
 

@@ -1,7 +1,9 @@
 // pt_abi.hip — the extern "C" boundary of libptmi.so (declared in
 // include/ptmi.h): argument validation, scene/frame conversion, launch of the
-// megakernel / wavefront / tone-map / clear kernels. No allocation and no
-// host synchronisation happens inside a render call (graph-capturable).
+// megakernel / wavefront / tone-map / clear kernels. No device allocation
+// happens inside a render call; the megakernel calls are asynchronous and
+// graph-capturable, the wavefront reads its live-slot count back every 8
+// iterations (one pinned 4-byte slot, allocated once).
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -9,16 +11,10 @@
 #include <cstring>
 #include <string>
 
-#include "pt_device.hpp"
+#include "pt_launch.hpp"
 #include "pt_prof.hpp"
 
 namespace ptmi {
-hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, float* accum,
-                     int32_t s_begin, int32_t s_count, unsigned long long* counters, hipStream_t stream);
-hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws, size_t ws_bytes,
-                     float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
-                     hipStream_t stream);
-size_t wf_workspace_bytes(int32_t npix, int32_t batch);
 
 // clear_accum_buffer, kernels.py:1205-1209 (restricted to the frame's pixel set).
 __global__ __launch_bounds__(kBlock) void clear_kernel(DevFrame fr, float* __restrict__ accum) {
@@ -184,6 +180,37 @@ int ptmi_mk_render(const ptmi_scene_view* scene, const ptmi_frame* frame, float*
   return check_hip(mk_render(sc, fr, stack_needed(scene), accum, sample_begin, sample_count,
                              (unsigned long long*)counters, (hipStream_t)stream),
                    "mk_render launch");
+}
+
+size_t ptmi_mk_workspace_bytes(const ptmi_frame* frame, int32_t batch_samples) {
+  DevFrame fr;
+  if (to_dev_frame(frame, fr)) return 0;
+  if (batch_samples <= 0) {
+    fail(PTMI_EINVAL, "batch_samples must be > 0");
+    return 0;
+  }
+  return mk_workspace_bytes(fr.w * fr.n_rows, batch_samples);
+}
+
+int ptmi_mk_render_ws(const ptmi_scene_view* scene, const ptmi_frame* frame, void* workspace,
+                      size_t workspace_bytes, float* accum, int32_t sample_begin, int32_t sample_count,
+                      uint64_t* counters, void* stream) {
+  DevScene sc;
+  DevFrame fr;
+  int rc = to_dev_scene(scene, sc);
+  if (rc) return rc;
+  if ((rc = to_dev_frame(frame, fr))) return rc;
+  if (!accum) return fail(PTMI_EINVAL, "accum is NULL");
+  if (sample_begin < 0 || sample_count < 0) return fail(PTMI_EINVAL, "bad sample range");
+  const int32_t npix = fr.w * fr.n_rows;
+  if (npix == 0) return PTMI_OK;
+  if (!workspace || !aligned16(workspace) || workspace_bytes < mk_workspace_bytes(npix, 1))
+    return fail(PTMI_EINVAL, "workspace too small/misaligned (%zu < %zu)", workspace_bytes,
+                mk_workspace_bytes(npix, 1));
+  if (sample_count == 0) return PTMI_OK;
+  return check_hip(mk_render_staged(sc, fr, stack_needed(scene), workspace, workspace_bytes, accum, sample_begin,
+                                    sample_count, (unsigned long long*)counters, (hipStream_t)stream),
+                   "mk_render_ws");
 }
 
 size_t ptmi_wf_workspace_bytes(const ptmi_frame* frame, int32_t batch_samples) {

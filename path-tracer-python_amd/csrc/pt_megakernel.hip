@@ -10,9 +10,15 @@
 //     constant-medium exit search (kernels.py:417) is not a nested second
 //     traversal but its own iteration (mode MEDIUM_EXIT), so lanes doing it
 //     share the traversal code with lanes tracing ordinary segments;
-//   * the accumulator is read once and written once per launch (sample
-//     colours added in sample order in registers: same float sequence as
-//     accum += color per sample);
+//   * direct mode: the accumulator is read once and written once per launch
+//     (sample colours added in sample order in registers: same float
+//     sequence as accum += color per sample);
+//   * staged mode (the default for multi-sample calls): work units are
+//     (tile, chunk of samples), many more than the chip holds at once, so the
+//     launch does not end in a long partially-filled last round of blocks
+//     (one unit per tile left ~30 % of the chip idle in the tail); each path
+//     writes its colour to staging[sample][pixel] and stage_resolve adds
+//     them in sample order — the same float additions as direct mode;
 //   * BVH: child-box BVH2 nodes (64 B, one node load tests both children),
 //     traversal stack in LDS (slot-major, conflict-free), see pt_device.hpp.
 // Perlin corner loop fully unrolled here (A/B on MI355X: +2.5 % megakernel,
@@ -20,7 +26,7 @@
 #ifndef PTMI_PERLIN_UNROLL
 #define PTMI_PERLIN_UNROLL 2
 #endif
-#include "pt_device.hpp"
+#include "pt_launch.hpp"
 #include "pt_prof.hpp"
 
 namespace ptmi {
@@ -55,10 +61,10 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
 
-template <int STACK>
-__global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(DevScene sc, DevFrame fr, float* __restrict__ accum,
-                                                           int32_t s_begin, int32_t s_count,
-                                                           unsigned long long* __restrict__ counters) {
+template <int STACK, bool STAGED>
+__global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
+    DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
+    float* __restrict__ staging, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
@@ -76,9 +82,17 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
   pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
   float* ap = nullptr;
   int32_t s = s_begin, s_end = s_begin + s_count;
+  if (STAGED) {  // this block's chunk of the call's samples
+    s = s_begin + (int32_t)blockIdx.z * chunk;
+    s_end = min(s + chunk, s_begin + s_count);
+    const size_t npix = (size_t)fr.w * (size_t)fr.n_rows;
+    ap = staging + 3 * ((size_t)(s - s_begin) * npix + (size_t)lr * (size_t)fr.w + (size_t)(px - fr.x0));
+  }
   if (valid) {
-    ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
-    acc = pt_v3f(ap[0], ap[1], ap[2]);
+    if (!STAGED) {
+      ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
+      acc = pt_v3f(ap[0], ap[1], ap[2]);
+    }
   } else {
     s = s_end;
   }
@@ -172,13 +186,20 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
       }
     }
     if (done) {
-      acc = pt_add(acc, ps.color);  // render_sample: accum += color (kernels.py:1187)
+      if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
+        ap[0] = ps.color.x;
+        ap[1] = ps.color.y;
+        ap[2] = ps.color.z;
+        ap += 3 * (size_t)fr.w * (size_t)fr.n_rows;
+      } else {
+        acc = pt_add(acc, ps.color);  // render_sample: accum += color (kernels.py:1187)
+      }
       ++n_paths;
       ++s;
       if (s < s_end) start_path(fr, px, py, s, ps);
     }
   }
-  if (valid) {
+  if (valid && !STAGED) {
     ap[0] = acc.x;
     ap[1] = acc.y;
     ap[2] = acc.z;
@@ -196,13 +217,46 @@ __global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void
   }
 }
 
+// accum[pixel] += staging[s][p] for s = 0..batch-1 in order (render_sample's
+// per-sample accumulation, kernels.py:1187 / renderer.py:405).
+__global__ __launch_bounds__(kBlock) void stage_resolve(DevFrame fr, const float* __restrict__ staging, int32_t npix,
+                                                        int32_t batch, float* __restrict__ accum) {
+  for (int32_t p = (int32_t)(blockIdx.x * kBlock + threadIdx.x); p < npix; p += (int32_t)(gridDim.x * kBlock)) {
+    int32_t lr = p / fr.w;
+    int32_t px = fr.x0 + (p - lr * fr.w);
+    int32_t py = frame_row(fr, lr);
+    float* ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
+    float a0 = ap[0], a1 = ap[1], a2 = ap[2];
+    const float* sp = staging + 3 * (size_t)p;
+    for (int32_t s = 0; s < batch; ++s) {
+      const float* c = sp + 3 * (size_t)s * (size_t)npix;
+      a0 += c[0];
+      a1 += c[1];
+      a2 += c[2];
+    }
+    ap[0] = a0;
+    ap[1] = a1;
+    ap[2] = a2;
+  }
+}
+
+hipError_t launch_stage_resolve(const DevFrame& fr, const float* staging, int32_t npix, int32_t batch,
+                                float* accum, int prof_kind, hipStream_t stream) {
+  unsigned g = (unsigned)((npix + kBlock - 1) / kBlock);
+  if (g > 2048) g = 2048;
+  prof_begin(prof_kind, stream);
+  hipLaunchKernelGGL(stage_resolve, dim3(g), dim3(kBlock), 0, stream, fr, staging, npix, batch, accum);
+  prof_end(prof_kind, stream);
+  return hipGetLastError();
+}
+
 template <int STACK>
 static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum, int32_t s_begin,
                             int32_t s_count, unsigned long long* counters, hipStream_t stream) {
   dim3 grid((unsigned)((fr.w + 15) / 16), (unsigned)((fr.n_rows + 15) / 16));
   prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL(mk_render_kernel<STACK>, grid, dim3(kBlock), 0, stream, sc, fr, accum, s_begin, s_count,
-                     counters);
+  hipLaunchKernelGGL((mk_render_kernel<STACK, false>), grid, dim3(kBlock), 0, stream, sc, fr, accum, s_begin,
+                     s_count, s_count, (float*)nullptr, counters);
   prof_end(kProfMk, stream);
   return hipGetLastError();
 }
@@ -213,6 +267,55 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
   if (stack_needed <= 24) return launch_mk<24>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 32) return launch_mk<32>(sc, fr, accum, s_begin, s_count, counters, stream);
   return launch_mk<64>(sc, fr, accum, s_begin, s_count, counters, stream);
+}
+
+// ---------------------------------------------------------------- staged
+#ifndef PTMI_MK_TARGET_BLOCKS
+#define PTMI_MK_TARGET_BLOCKS 16384  // ~16 rounds of 4 blocks x 256 CUs
+#endif
+
+size_t mk_workspace_bytes(int32_t npix, int32_t batch) {
+  if (npix <= 0 || batch <= 0) return 0;
+  return (3 * sizeof(float) * (size_t)npix * (size_t)batch + 255) & ~(size_t)255;
+}
+
+template <int STACK>
+static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float* staging, float* accum,
+                                   int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream) {
+  const unsigned tx = (unsigned)((fr.w + 15) / 16), ty = (unsigned)((fr.n_rows + 15) / 16);
+  const int64_t tiles = (int64_t)tx * ty;
+  int64_t nchunks = (PTMI_MK_TARGET_BLOCKS + tiles - 1) / tiles;
+  if (nchunks < 1) nchunks = 1;
+  if (nchunks > nb) nchunks = nb;
+  const int32_t chunk = (int32_t)((nb + nchunks - 1) / nchunks);
+  nchunks = (nb + chunk - 1) / chunk;
+  prof_begin(kProfMk, stream);
+  hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3(tx, ty, (unsigned)nchunks), dim3(kBlock), 0, stream,
+                     sc, fr, accum, s_begin, nb, chunk, staging, counters);
+  prof_end(kProfMk, stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_stage_resolve(fr, staging, fr.w * fr.n_rows, nb, accum, kProfMkResolve, stream);
+}
+
+hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
+                            size_t ws_bytes, float* accum, int32_t s_begin, int32_t s_count,
+                            unsigned long long* counters, hipStream_t stream) {
+  const int32_t npix = fr.w * fr.n_rows;
+  int32_t batch = s_count;
+  while (batch > 1 && mk_workspace_bytes(npix, batch) > ws_bytes) batch = (batch + 1) / 2;
+  if (mk_workspace_bytes(npix, batch) > ws_bytes) return hipErrorInvalidValue;
+  for (int32_t b0 = 0; b0 < s_count; b0 += batch) {
+    const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
+    float* st = (float*)ws;
+    hipError_t e;
+    if (stack_needed <= 16) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    else if (stack_needed <= 24) e = launch_mk_staged<24>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    else if (stack_needed <= 32) e = launch_mk_staged<32>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    else e = launch_mk_staged<64>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace ptmi

@@ -5,7 +5,7 @@
 
 namespace ptmi {
 enum : int32_t { kProfMk = 0, kProfWfGenerate = 1, kProfWfIntersect = 2, kProfWfShade = 3, kProfWfMedium = 4,
-                 kProfWfResolve = 5, kProfKinds = 6 };
+                 kProfWfResolve = 5, kProfMkResolve = 6, kProfKinds = 7 };
 void prof_begin(int32_t kind, hipStream_t s);
 void prof_end(int32_t kind, hipStream_t s);
 int prof_start(int32_t max_launches);

@@ -33,7 +33,7 @@
 //     accumulator in sample order — the same float additions, in the same
 //     order, as the reference's per-sample accumulation, with no atomics and
 //     no ordering constraint between concurrent paths of one pixel.
-#include "pt_device.hpp"
+#include "pt_launch.hpp"
 #include "pt_prof.hpp"
 
 namespace ptmi {
@@ -411,29 +411,6 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
   if (counters) block_flush(n_ended, lds_stack, counters + 2);
 }
 
-// accum[pixel] += staging[s][p] for s = 0..batch-1 in order (render_sample's
-// per-sample accumulation, kernels.py:1187 / renderer.py:305).
-__global__ __launch_bounds__(kBlock) void wf_resolve(DevFrame fr, WfBufs wb, int32_t batch,
-                                                     float* __restrict__ accum) {
-  for (int32_t p = (int32_t)(blockIdx.x * kBlock + threadIdx.x); p < wb.npix; p += (int32_t)(gridDim.x * kBlock)) {
-    int32_t lr = p / fr.w;
-    int32_t px = fr.x0 + (p - lr * fr.w);
-    int32_t py = frame_row(fr, lr);
-    float* ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
-    float a0 = ap[0], a1 = ap[1], a2 = ap[2];
-    const float* sp = wb.staging + 3 * (size_t)p;
-    for (int32_t s = 0; s < batch; ++s) {
-      const float* c = sp + 3 * (size_t)s * (size_t)wb.npix;
-      a0 += c[0];
-      a1 += c[1];
-      a2 += c[2];
-    }
-    ap[0] = a0;
-    ap[1] = a1;
-    ap[2] = a2;
-  }
-}
-
 namespace {
 int32_t* g_pinned_live = nullptr;  // host-pinned readback slot for the live-slot count
 #ifndef PTMI_WF_CAPACITY_LOG2
@@ -508,12 +485,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, fl
     if (e != hipSuccess) return e;
     if (*g_pinned_live == 0) break;
   }
-  prof_begin(kProfWfResolve, stream);
-  unsigned gr = (unsigned)((wb.npix + kBlock - 1) / kBlock);
-  if (gr > 2048) gr = 2048;
-  hipLaunchKernelGGL(wf_resolve, dim3(gr), dim3(kBlock), 0, stream, fr, wb, batch, accum);
-  prof_end(kProfWfResolve, stream);
-  return hipGetLastError();
+  return launch_stage_resolve(fr, wb.staging, wb.npix, batch, accum, kProfWfResolve, stream);
 }
 
 size_t wf_workspace_bytes(int32_t npix, int32_t batch) {

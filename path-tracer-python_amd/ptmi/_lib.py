@@ -11,6 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PTMI_LIB') or os.path.join(_HERE, '_lib', 'libptmi.so')  # PTMI_LIB: A/B builds
+ABI_VERSION = 2  # PTMI_ABI_VERSION of include/ptmi.h
 MAX_IMAGES = 16
 NUM_COUNTERS = 4
 
@@ -44,10 +45,11 @@ class Frame(C.Structure):
                 ('band_rows', C.c_int32), ('band_stride', C.c_int32), ('band_offset', C.c_int32)]
 
 
-EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_wf_workspace_bytes',
+EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',
+           'ptmi_mk_render_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
            'ptmi_prof_stop')
-PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve')
+PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve', 'mk_resolve')
 
 _lib = None
 
@@ -70,6 +72,10 @@ def load(path: str = LIB_PATH):
     lib.ptmi_last_error.restype = C.c_char_p
     lib.ptmi_scene_check.argtypes = [C.POINTER(SceneView)]
     lib.ptmi_mk_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_int32, C.c_int32, P, P]
+    lib.ptmi_mk_workspace_bytes.argtypes = [C.POINTER(Frame), C.c_int32]
+    lib.ptmi_mk_workspace_bytes.restype = C.c_size_t
+    lib.ptmi_mk_render_ws.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,
+                                      C.c_int32, P, P]
     lib.ptmi_wf_workspace_bytes.argtypes = [C.POINTER(Frame), C.c_int32]
     lib.ptmi_wf_workspace_bytes.restype = C.c_size_t
     lib.ptmi_wf_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,
@@ -80,8 +86,8 @@ def load(path: str = LIB_PATH):
                                        C.POINTER(C.c_int32)]
     lib.ptmi_prof_start.argtypes = [C.c_int32]
     lib.ptmi_prof_stop.argtypes = [P, P, C.c_int32]
-    if lib.ptmi_version() != 1:
-        raise PtmiError('libptmi ABI version mismatch')
+    if lib.ptmi_version() != ABI_VERSION:
+        raise PtmiError(f'libptmi ABI version {lib.ptmi_version()} != {ABI_VERSION} (rebuild libptmi.so)')
     _lib = lib
     return lib
 

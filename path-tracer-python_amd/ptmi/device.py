@@ -126,22 +126,39 @@ class Integrator:
     def _cnt(self):
         return C.c_void_p(self.counters.data_ptr()) if self.counters is not None else None
 
-    def render_mk(self, frame, accum, sample_begin, sample_count, stream=None):
+    # multi-sample megakernel calls run as (tile, sample chunk) work units with
+    # staged colours (ptmi_mk_render_ws); single samples accumulate directly
+    MK_STAGED_MIN_SAMPLES = 2
+
+    def render_mk(self, frame, accum, sample_begin, sample_count, stream=None, staged=None):
         _check_accum(accum, frame)
+        if staged is None:
+            staged = int(sample_count) >= self.MK_STAGED_MIN_SAMPLES
+        if staged:
+            ws = self.workspace(frame, sample_count, 'mk')
+            _lib.check(self.lib.ptmi_mk_render_ws(C.byref(self.scene.view), C.byref(frame), C.c_void_p(ws.data_ptr()),
+                                                  self._ws_bytes, C.c_void_p(accum.data_ptr()), int(sample_begin),
+                                                  int(sample_count), self._cnt(), _stream_ptr(stream)),
+                       'ptmi_mk_render_ws')
+            return
         _lib.check(self.lib.ptmi_mk_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(accum.data_ptr()),
                                            int(sample_begin), int(sample_count), self._cnt(), _stream_ptr(stream)),
                    'ptmi_mk_render')
 
-    # staging budget for the wavefront's per-(sample, pixel) colour slots
-    WF_STAGING_BYTES = 1 << 30
+    # staging budget for the per-(sample, pixel) colour slots of one batch
+    STAGING_BYTES = 1 << 30
 
-    def workspace(self, frame, sample_count=1):
+    def workspace(self, frame, sample_count=1, kind='wf'):
+        """Cached device workspace (torch) big enough for one batch of the call
+        (shared by the megakernel's staged mode and the wavefront)."""
         npix = frame.w * len(frame_pixel_rows(frame))
-        batch = max(1, min(int(sample_count), self.WF_STAGING_BYTES // max(1, 12 * npix)))
-        need = int(self.lib.ptmi_wf_workspace_bytes(C.byref(frame), batch))
+        batch = max(1, min(int(sample_count), self.STAGING_BYTES // max(1, 12 * npix)))
+        fn = self.lib.ptmi_wf_workspace_bytes if kind == 'wf' else self.lib.ptmi_mk_workspace_bytes
+        need = int(fn(C.byref(frame), batch))
         if need == 0:
-            _lib.check(-1, 'ptmi_wf_workspace_bytes')
+            _lib.check(-1, f'ptmi_{kind}_workspace_bytes')
         if self._ws is None or self._ws_bytes < need:
+            self._ws = None
             self._ws = torch.empty((need + 15) // 16 * 4, dtype=torch.float32, device=self.scene.device)
             self._ws_bytes = self._ws.numel() * 4
         return self._ws

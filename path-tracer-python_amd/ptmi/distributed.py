@@ -51,7 +51,12 @@ def reduce_accum(accum, dst=0, group=None):
     """Sum-reduce the accumulator onto `dst` (in place); no-op for world 1."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.reduce(accum, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if accum.is_cuda and dist.get_backend(group) == 'gloo':  # rehearsal backend: reduce a host copy
+            host = accum.cpu()
+            dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            accum.copy_(host)
+        else:
+            dist.reduce(accum, dst=dst, op=dist.ReduceOp.SUM, group=group)
     return accum
 
 

@@ -83,3 +83,24 @@ def test_tonemap_matches_reference_formula():
         scale = 1.0 / max(1, spp)
         ref = np.clip(np.sqrt(np.maximum(0, acc * scale)) * 255.999, 0, 255).astype(np.uint8)
         assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize('band', [(1, 1, 0), (8, 2, 1)])
+def test_staged_megakernel_equals_direct(band):
+    """ptmi_mk_render_ws (tile x sample-chunk units, staged colours, ordered
+    resolve) is bit-identical to ptmi_mk_render (per-thread accumulation)."""
+    import torch
+    from ptmi import device
+    from parity_helpers import scene_inputs
+    sa, cam, bg = scene_inputs('vol2_final_scene', 800)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, 800, 800, (96, 200, 200, 136), band)
+    out = []
+    for staged in (False, True):
+        acc = torch.zeros((800, 800, 3), dtype=torch.float32, device='cuda')
+        acc[:] = 0.25  # accumulate onto a non-zero image
+        integ.render_mk(fr, acc, 3, 37, staged=staged)
+        integ.render_mk(fr, acc, 40, 5, staged=staged)
+        torch.cuda.synchronize()
+        out.append(acc.cpu().numpy())
+    assert np.array_equal(out[0], out[1])

@@ -26,7 +26,9 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) == set(_lib.EXPORTS)
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.ptmi_version() == 1
+    with open(os.path.join(ROOT, 'include', 'ptmi.h')) as f:
+        ver = int(re.search(r'#define PTMI_ABI_VERSION (\d+)', f.read()).group(1))
+    assert lib.ptmi_version() == ver == 2
 
 
 def test_struct_layouts_match_header():

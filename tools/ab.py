@@ -13,7 +13,8 @@ def main():
     integ = device.Integrator(device.DeviceScene.from_arrays(sa))
     fr = device.make_frame(cam, (0, 0, 0), 50, 0, 800, 800)
     acc = torch.zeros((800, 800, 3), dtype=torch.float32, device='cuda')
-    f = integ.render_mk if variant == 'mk' else integ.render_wf
+    f = {'mk': integ.render_mk, 'wf': integ.render_wf,
+         'mkd': lambda *a: integ.render_mk(*a, staged=False)}[variant]
     f(fr, acc, 0, 4); torch.cuda.synchronize()
     best = 1e9
     for r in range(reps):

@@ -42,6 +42,8 @@ for s in "$@"; do
                  "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_BUSY_CYCLES"; do
              n=$((n+1)); step pmcta_${v}$n 600 rocprofv3 --pmc $ps --output-format csv -d gpurun_out/pmcta -o ${v}$n -- python tools/ab.py $v 64 1 || exit 1
            done; done ;;
+    dist2) step dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 ;;
+    dist2t) step dist2t 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --shard tiles ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s" ;;
   esac
