@@ -443,6 +443,11 @@ Layout layout(int32_t npix, int32_t batch) {
 }
 }  // namespace
 
+#ifndef PTMI_WF_MAX_BLOCKS
+#define PTMI_WF_MAX_BLOCKS 2048  // multiple of kShards
+#endif
+static_assert(PTMI_WF_MAX_BLOCKS % kShards == 0, "grid must be a multiple of the shard count");
+
 template <int STACK>
 static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, float* accum, int32_t batch,
                            unsigned long long* counters, hipStream_t stream) {
@@ -452,7 +457,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, fl
   // grid = multiple of kShards and of the slot quantum, so slot i always maps
   // to block (i / kBlock) % grid with shard (i / kBlock) % kShards
   int64_t blocks = wb.capacity / kBlock;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > PTMI_WF_MAX_BLOCKS) blocks = PTMI_WF_MAX_BLOCKS;
   const unsigned g = (unsigned)blocks;
   (void)hipMemsetAsync(wb.ctl, 0, kCtlWords * sizeof(int32_t), stream);
   prof_begin(kProfWfGenerate, stream);
