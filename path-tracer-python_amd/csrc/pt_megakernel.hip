@@ -62,7 +62,9 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #endif
 
 template <int STACK, bool STAGED>
-__global__ __launch_bounds__(kBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
+// waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
+// (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the 4-wave VGPR budget of 128
+__global__ __launch_bounds__(kBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kBlock];
@@ -264,6 +266,7 @@ static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum
 hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, float* accum,
                      int32_t s_begin, int32_t s_count, unsigned long long* counters, hipStream_t stream) {
   if (stack_needed <= 16) return launch_mk<16>(sc, fr, accum, s_begin, s_count, counters, stream);
+  if (stack_needed <= 20) return launch_mk<20>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 24) return launch_mk<24>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 32) return launch_mk<32>(sc, fr, accum, s_begin, s_count, counters, stream);
   return launch_mk<64>(sc, fr, accum, s_begin, s_count, counters, stream);
@@ -301,6 +304,9 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
 hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
                             size_t ws_bytes, float* accum, int32_t s_begin, int32_t s_count,
                             unsigned long long* counters, hipStream_t stream) {
+  const int64_t tiles = (int64_t)((fr.w + 15) / 16) * ((fr.n_rows + 15) / 16);
+  if (tiles >= PTMI_MK_TARGET_BLOCKS / 2 || s_count < 2)  // the tiles alone fill the chip: no staging
+    return mk_render(sc, fr, stack_needed, accum, s_begin, s_count, counters, stream);
   const int32_t npix = fr.w * fr.n_rows;
   int32_t batch = s_count;
   while (batch > 1 && mk_workspace_bytes(npix, batch) > ws_bytes) batch = (batch + 1) / 2;
@@ -310,6 +316,7 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
     float* st = (float*)ws;
     hipError_t e;
     if (stack_needed <= 16) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    else if (stack_needed <= 20) e = launch_mk_staged<20>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 24) e = launch_mk_staged<24>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 32) e = launch_mk_staged<32>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else e = launch_mk_staged<64>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);

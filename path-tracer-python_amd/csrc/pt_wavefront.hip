@@ -530,6 +530,7 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     wb.s_begin = s_begin + b0;
     hipError_t e;
     if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wb, accum, nb, counters, stream);
+    else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wb, accum, nb, counters, stream);
     else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wb, accum, nb, counters, stream);
     else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wb, accum, nb, counters, stream);
     else e = wf_batch<64>(sc, fr, wb, accum, nb, counters, stream);

@@ -14,8 +14,8 @@ fi
 for round in 1 2; do
   for v in ${AB_MODES:-mk wf}; do
     for lib in "${libs[@]}"; do
-      PTMI_LIB=$PWD/$lib timeout -k 10 120 python tools/ab.py $v 64 ${AB_REPS:-4} >> gpurun_out/ab.log 2>&1 || { echo "$lib $v failed rc=$?"; exit 1; }
+      PTMI_LIB=$PWD/$lib timeout -k 10 120 python tools/ab.py $v ${AB_SPP:-64} ${AB_REPS:-4} ${AB_SCENE:-vol2_final_scene} ${AB_WIDTH:-800} >> gpurun_out/ab_runs.log 2>&1 || { echo "$lib $v failed rc=$?"; exit 1; }
     done
   done
 done
-cp gpurun_out/ab.log /tmp/ab_copy.log; grep -h Msamples /tmp/ab_copy.log
+cp gpurun_out/ab_runs.log /tmp/ab_copy.log; grep -h Msamples /tmp/ab_copy.log
