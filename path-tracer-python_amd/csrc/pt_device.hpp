@@ -244,7 +244,7 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
 struct Stack {
-  uint2* slot0;  // &lds[tid]; slot k at slot0[k * kBlock]
+  uint2* slot0;  // &lds[tid]; slot k at slot0[k * SB] (SB = threads per block)
 };
 
 __device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz, float mxx, float mxy,
@@ -262,7 +262,7 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 #define PTMI_NODES_VGPR 1  // A/B on MI355X: +2 % megakernel
 #endif
 
-template <int STACK>
+template <int STACK, int SB = kBlock>
 __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
                                          float& t_out, int32_t& ref_out) {
   const pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
@@ -301,7 +301,7 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
   }
   while (sp > 0) {
     --sp;
-    const uint2 ent = st.slot0[sp * kBlock];
+    const uint2 ent = st.slot0[sp * SB];
     const int32_t ref = (int32_t)ent.x;
     if (!(__uint_as_float(ent.y) <= closest)) continue;
     if (ref < 0) {  // leaf: kernels.py:671-697
@@ -338,11 +338,11 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
     const bool h0 = X0 >= E0, h1 = X1 >= E1;
     const bool fh = ln ? h1 : h0, nh = ln ? h0 : h1;
     if (fh && sp < STACK) {  // far first
-      st.slot0[sp * kBlock] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+      st.slot0[sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
       ++sp;
     }
     if (nh && sp < STACK) {
-      st.slot0[sp * kBlock] = make_uint2((uint32_t)nr, __float_as_uint(nE));
+      st.slot0[sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
       ++sp;
     }
   }

@@ -61,23 +61,31 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
 
+// Block = PTMI_MK_BLOCK_WAVES waves: 4 -> a 16x16 pixel tile, 1 -> 8x8.
+#ifndef PTMI_MK_BLOCK_WAVES
+#define PTMI_MK_BLOCK_WAVES 1  // A/B on MI355X: 1-wave blocks +7 % (C2) / +12 % (C4): a finished wave frees its slot at once
+#endif
+constexpr int kMkBlock = 64 * PTMI_MK_BLOCK_WAVES;
+constexpr int kMkTile = PTMI_MK_BLOCK_WAVES == 4 ? 16 : 8;
+static_assert(PTMI_MK_BLOCK_WAVES == 4 || PTMI_MK_BLOCK_WAVES == 1, "block = 1 or 4 waves");
+
 template <int STACK, bool STAGED>
 // waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
 // (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the 4-wave VGPR budget of 128
-__global__ __launch_bounds__(kBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
+__global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters) {
-  __shared__ uint2 lds_stack[STACK * kBlock];
+  __shared__ uint2 lds_stack[STACK * kMkBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
 
-  // 16x16 pixel block = 4 waves of 8x8 (square footprints keep a wave's
-  // camera rays coherent in the BVH).
+  // each wave renders an 8x8 pixel square (square footprints keep a wave's
+  // camera rays coherent in the BVH); a 4-wave block covers 16x16.
   const int lane = tid & 63, wv = tid >> 6;
   const int32_t lx = ((wv & 1) << 3) | (lane & 7);
   const int32_t ly = ((wv >> 1) << 3) | (lane >> 3);
-  const int32_t px = fr.x0 + (int32_t)blockIdx.x * 16 + lx;
-  const int32_t lr = (int32_t)blockIdx.y * 16 + ly;
+  const int32_t px = fr.x0 + (int32_t)blockIdx.x * kMkTile + lx;
+  const int32_t lr = (int32_t)blockIdx.y * kMkTile + ly;
   int32_t py = (lr < fr.n_rows) ? frame_row(fr, lr) : -1;
   const bool valid = (px < fr.x0 + fr.w) && (py >= 0);
 
@@ -109,7 +117,7 @@ __global__ __launch_bounds__(kBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void
     const float tmin = exit_mode ? ps.t_entry + 0.0001f : kTMin;  // kernels.py:418 / 1057
     float t;
     int32_t ref;
-    bool hit = traverse<STACK>(sc, ps.o, ps.dir, tmin, kTMax, st, t, ref);
+    bool hit = traverse<STACK, kMkBlock>(sc, ps.o, ps.dir, tmin, kTMax, st, t, ref);
     if (exit_mode) ++n_med; else ++n_seg;
 
     bool done = false, scattered = false, passthrough = false;
@@ -255,9 +263,9 @@ hipError_t launch_stage_resolve(const DevFrame& fr, const float* staging, int32_
 template <int STACK>
 static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum, int32_t s_begin,
                             int32_t s_count, unsigned long long* counters, hipStream_t stream) {
-  dim3 grid((unsigned)((fr.w + 15) / 16), (unsigned)((fr.n_rows + 15) / 16));
+  dim3 grid((unsigned)((fr.w + kMkTile - 1) / kMkTile), (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile));
   prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, false>), grid, dim3(kBlock), 0, stream, sc, fr, accum, s_begin,
+  hipLaunchKernelGGL((mk_render_kernel<STACK, false>), grid, dim3(kMkBlock), 0, stream, sc, fr, accum, s_begin,
                      s_count, s_count, (float*)nullptr, counters);
   prof_end(kProfMk, stream);
   return hipGetLastError();
@@ -274,7 +282,7 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
 
 // ---------------------------------------------------------------- staged
 #ifndef PTMI_MK_TARGET_BLOCKS
-#define PTMI_MK_TARGET_BLOCKS 16384  // ~16 rounds of 4 blocks x 256 CUs
+#define PTMI_MK_TARGET_BLOCKS (16384 * 4 / PTMI_MK_BLOCK_WAVES)  // ~16 rounds of the chip's wave slots
 #endif
 
 size_t mk_workspace_bytes(int32_t npix, int32_t batch) {
@@ -285,7 +293,7 @@ size_t mk_workspace_bytes(int32_t npix, int32_t batch) {
 template <int STACK>
 static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float* staging, float* accum,
                                    int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream) {
-  const unsigned tx = (unsigned)((fr.w + 15) / 16), ty = (unsigned)((fr.n_rows + 15) / 16);
+  const unsigned tx = (unsigned)((fr.w + kMkTile - 1) / kMkTile), ty = (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile);
   const int64_t tiles = (int64_t)tx * ty;
   int64_t nchunks = (PTMI_MK_TARGET_BLOCKS + tiles - 1) / tiles;
   if (nchunks < 1) nchunks = 1;
@@ -293,7 +301,7 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   const int32_t chunk = (int32_t)((nb + nchunks - 1) / nchunks);
   nchunks = (nb + chunk - 1) / chunk;
   prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3(tx, ty, (unsigned)nchunks), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3(tx, ty, (unsigned)nchunks), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, chunk, staging, counters);
   prof_end(kProfMk, stream);
   hipError_t e = hipGetLastError();
@@ -304,7 +312,7 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
 hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
                             size_t ws_bytes, float* accum, int32_t s_begin, int32_t s_count,
                             unsigned long long* counters, hipStream_t stream) {
-  const int64_t tiles = (int64_t)((fr.w + 15) / 16) * ((fr.n_rows + 15) / 16);
+  const int64_t tiles = (int64_t)((fr.w + kMkTile - 1) / kMkTile) * ((fr.n_rows + kMkTile - 1) / kMkTile);
   if (tiles >= PTMI_MK_TARGET_BLOCKS / 2 || s_count < 2)  // the tiles alone fill the chip: no staging
     return mk_render(sc, fr, stack_needed, accum, s_begin, s_count, counters, stream);
   const int32_t npix = fr.w * fr.n_rows;
