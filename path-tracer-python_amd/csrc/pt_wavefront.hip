@@ -39,6 +39,10 @@
 namespace ptmi {
 
 constexpr int kShards = 8;
+#ifndef PTMI_WF_BLOCK
+#define PTMI_WF_BLOCK 256  // threads per block of the queue kernels
+#endif
+constexpr int kWfBlock = PTMI_WF_BLOCK;
 constexpr uint32_t kDead = 0xffffffffu;  // item of an empty slot
 
 struct Queue {
@@ -53,7 +57,7 @@ struct WfBufs {
   int32_t* medq;      // kShards segments of medseg slot indices
   float* staging;     // [batch][npix][3] path colours
   int32_t* ctl;       // kCtlWords counters, one per 256-B line (see ctl_*)
-  int32_t capacity;   // queue slots (multiple of kShards * kBlock)
+  int32_t capacity;   // queue slots (multiple of kShards * kWfBlock)
   int32_t medseg;     // slots per shard
   int32_t npix;       // pixels of the frame's pixel set
   int32_t total;      // work items of the batch (= batch samples * npix)
@@ -75,10 +79,10 @@ __host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
-// Slot i is processed by block (i / kBlock) % grid, grid a multiple of kShards.
-__device__ __forceinline__ int32_t slot_shard(int32_t i) { return (i / kBlock) % kShards; }
+// Slot i is processed by block (i / kWfBlock) % grid, grid a multiple of kShards.
+__device__ __forceinline__ int32_t slot_shard(int32_t i) { return (i / kWfBlock) % kShards; }
 __device__ __forceinline__ int32_t slot_rank(int32_t i) {  // index of slot i among its shard's slots
-  return ((i / kBlock) / kShards) * kBlock + (i % kBlock);
+  return ((i / kWfBlock) / kShards) * kWfBlock + (i % kWfBlock);
 }
 
 // Wave-aggregated counter increment: this lane's ticket (meaningful only if want).
@@ -190,8 +194,8 @@ __device__ __forceinline__ int32_t shard_end(const WfBufs& wb, int32_t s) {
 }
 
 // Initial fill: the r-th slot of shard s takes item s*shard_len + r.
-__global__ __launch_bounds__(kBlock) void wf_generate(DevFrame fr, WfBufs wb) {
-  for (int32_t i = (int32_t)(blockIdx.x * kBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kBlock)) {
+__global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb) {
+  for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kWfBlock)) {
     const int32_t s = slot_shard(i);
     const int64_t k = (int64_t)s * wb.shard_len + slot_rank(i);
     const bool live = slot_rank(i) < wb.shard_len && k < shard_end(wb, s);
@@ -208,23 +212,23 @@ __global__ __launch_bounds__(kBlock) void wf_generate(DevFrame fr, WfBufs wb) {
 
 // intersect_rays, kernels.py:1242-1263.
 template <int STACK>
-__global__ __launch_bounds__(kBlock) void wf_intersect(DevScene sc, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, WfBufs wb,
                                                        unsigned long long* __restrict__ counters) {
-  __shared__ uint2 lds_stack[STACK * kBlock];
+  __shared__ uint2 lds_stack[STACK * kWfBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
   if (blockIdx.x < kShards && tid == 0) *ctl_medium(wb, blockIdx.x) = 0;  // medium counts of this iteration
   const Queue q = wb.q;
-  const int32_t stride = (int32_t)(gridDim.x * kBlock);
+  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_live = 0;
-  for (int32_t i = (int32_t)(blockIdx.x * kBlock + tid); i < wb.capacity; i += stride) {
+  for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + tid); i < wb.capacity; i += stride) {
     if (slot_item(q, i) == kDead) continue;
     ++n_live;
     float4 a = q.a[i], b = q.b[i];
     pt_v3 o = pt_v3f(a.x, a.y, a.z), d = pt_v3f(a.w, b.x, b.y);
     float t;
     int32_t ref;
-    bool hit = traverse<STACK>(sc, o, d, kTMin, kTMax, st, t, ref);
+    bool hit = traverse<STACK, kWfBlock>(sc, o, d, kTMin, kTMax, st, t, ref);
     wb.hit[i] = make_float2(t, __int_as_float(hit ? ref : kMissRef));
   }
   if (counters) block_flush(n_live, lds_stack, counters + 0);
@@ -280,15 +284,15 @@ __device__ __forceinline__ void finish_lane(const DevFrame& fr, const WfBufs& wb
 
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
 // medium-boundary hits go to their shard's medium queue segment.
-__global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
                                                    unsigned long long* __restrict__ counters) {
   const Queue q = wb.q;
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
-  const int32_t stride = (int32_t)(gridDim.x * kBlock);
+  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
   __shared__ unsigned int tally;
   uint32_t n_ended = 0;
-  for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < wb.capacity; base += stride) {
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < wb.capacity; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
     bool to_medium = false, ended = false, go = false;
     Ray cont;
@@ -334,9 +338,9 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, DevFrame fr, WfB
 // kernels.py:365-450) and the volume branch of shade_and_scatter
 // (kernels.py:1326-1357). Work index j runs over the concatenated shard segments.
 template <int STACK>
-__global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
                                                     unsigned long long* __restrict__ counters) {
-  __shared__ uint2 lds_stack[STACK * kBlock];
+  __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
   int32_t cnt[kShards];  // per-shard medium counts (wave-uniform)
   int32_t n = 0;
@@ -346,9 +350,9 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
     n += cnt[s];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
-  const int32_t stride = (int32_t)(gridDim.x * kBlock);
+  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0;
-  for (int32_t base = (int32_t)(blockIdx.x * kBlock); base < n; base += stride) {
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
     Ray cont;
@@ -369,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void wf_medium(DevScene sc, DevFrame fr, Wf
       const float t_entry = h.x;
       float te;
       int32_t rex;
-      const bool hx = traverse<STACK>(sc, ray.o, ray.d, t_entry + 0.0001f, kTMax, st, te, rex);
+      const bool hx = traverse<STACK, kWfBlock>(sc, ray.o, ray.d, t_entry + 0.0001f, kTMax, st, te, rex);
       const Mat m = load_mat(sc, mat_index(sc, ref));
       Item it = decode_item(fr, wb, ray.item);
       Rng r{path_key(fr, wb, it), ray.ctr};
@@ -417,7 +421,7 @@ int32_t* g_pinned_live = nullptr;  // host-pinned readback slot for the live-slo
 #define PTMI_WF_CAPACITY_LOG2 20
 #endif
 constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
-constexpr int32_t kSlotQuantum = kShards * kBlock;
+constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
 struct Layout {
   int32_t capacity, medseg;
@@ -444,7 +448,7 @@ Layout layout(int32_t npix, int32_t batch) {
 }  // namespace
 
 #ifndef PTMI_WF_MAX_BLOCKS
-#define PTMI_WF_MAX_BLOCKS 2048  // multiple of kShards
+#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // multiple of kShards
 #endif
 static_assert(PTMI_WF_MAX_BLOCKS % kShards == 0, "grid must be a multiple of the shard count");
 
@@ -455,13 +459,13 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, fl
   counters = nullptr;  // A/B only: prices the statistics atomics
 #endif
   // grid = multiple of kShards and of the slot quantum, so slot i always maps
-  // to block (i / kBlock) % grid with shard (i / kBlock) % kShards
-  int64_t blocks = wb.capacity / kBlock;
+  // to block (i / kWfBlock) % grid with shard (i / kWfBlock) % kShards
+  int64_t blocks = wb.capacity / kWfBlock;
   if (blocks > PTMI_WF_MAX_BLOCKS) blocks = PTMI_WF_MAX_BLOCKS;
   const unsigned g = (unsigned)blocks;
   (void)hipMemsetAsync(wb.ctl, 0, kCtlWords * sizeof(int32_t), stream);
   prof_begin(kProfWfGenerate, stream);
-  hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kBlock), 0, stream, fr, wb);
+  hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kWfBlock), 0, stream, fr, wb);
   prof_end(kProfWfGenerate, stream);
   // Each item needs at most max_depth waves and every iteration advances every
   // live ray by one wave, so total * max_depth iterations always drain the pool.
@@ -472,13 +476,13 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, fl
     int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
       prof_begin(kProfWfIntersect, stream);
-      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, wb, counters);
+      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kWfBlock), 0, stream, sc, wb, counters);
       prof_end(kProfWfIntersect, stream);
       prof_begin(kProfWfShade, stream);
-      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, counters);
+      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
       prof_end(kProfWfShade, stream);
       prof_begin(kProfWfMedium, stream);
-      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kBlock), 0, stream, sc, fr, wb, counters);
+      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
       prof_end(kProfWfMedium, stream);
     }
     it += n;
