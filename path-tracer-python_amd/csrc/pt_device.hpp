@@ -258,6 +258,10 @@ __device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, f
 
 __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 
+#ifndef PTMI_PUSH_BRANCHFREE
+#define PTMI_PUSH_BRANCHFREE 1
+#endif
+
 #ifndef PTMI_NODES_VGPR
 #define PTMI_NODES_VGPR 1  // A/B on MI355X: +2 % megakernel
 #endif
@@ -337,6 +341,17 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
     const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
     const bool h0 = X0 >= E0, h1 = X1 >= E1;
     const bool fh = ln ? h1 : h0, nh = ln ? h0 : h1;
+#if PTMI_PUSH_BRANCHFREE
+    // Far first, then near; each slot written unconditionally and kept only if
+    // its child is hit. No bound check: an internal node at depth d has at most
+    // d pending entries, so sp + 2 <= max_leaf_depth + 1 <= STACK always
+    // (STACK >= max_leaf_depth + 1 is enforced at dispatch) and the
+    // reference's overflow drop can never trigger.
+    st.slot0[sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+    sp += fh ? 1 : 0;
+    st.slot0[sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
+    sp += nh ? 1 : 0;
+#else
     if (fh && sp < STACK) {  // far first
       st.slot0[sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
       ++sp;
@@ -345,6 +360,7 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
       st.slot0[sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
       ++sp;
     }
+#endif
   }
   t_out = closest;
   ref_out = best;

@@ -36,7 +36,7 @@ for s in "$@"; do
                  "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum" "TCP_TCC_ATOMIC_WITH_RET_REQ_sum TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum"; do
              n=$((${n:-0}+1)); step pmcwf$n 600 rocprofv3 --pmc $ps --output-format csv -d gpurun_out/pmcwf -o p$n -- python tools/ab.py wf 64 1 || exit 1
            done ;;
-    pmcta) for v in mk wf; do n=0; for ps in "TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE" \
+    pmcta) for v in ${PMC_MODES:-mk wf}; do n=0; for ps in "TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE" \
                  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" "TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum" \
                  "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum" \
                  "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_BUSY_CYCLES"; do
