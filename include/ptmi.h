@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 2
+#define PTMI_ABI_VERSION 3
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -35,11 +35,12 @@ enum {
  * (scene_compiler.py:931 compile_scene + bvh_compiler.py:132 compile_bvh;
  * replaces the field uploads of renderer.py:102-228 / fields.py:25-153).
  * Layouts (all little-endian, 16-byte aligned):
- *   nodes   : n_inner x 16 f32 — internal BVH2 node holding BOTH children's
- *             boxes, interleaved per component so the two children form
- *             packed-f32 pairs: {min.x c0,c1, min.y c0,c1 | min.z c0,c1,
- *             max.x c0,c1 | max.y c0,c1, max.z c0,c1 | ref0, ref1, 0, 0
- *             (as i32 bits)}.
+ *   nodes   : n_inner x 20 f32 (80 B) — internal BVH2 node holding BOTH
+ *             children's boxes, interleaved per component so the two
+ *             children form packed-f32 pairs: {min.x c0,c1, min.y c0,c1 |
+ *             min.z c0,c1, max.x c0,c1 | max.y c0,c1, max.z c0,c1 |
+ *             ref0, ref1 (i32 bits), centre.z c0,c1 | centre.x c0,c1,
+ *             centre.y c0,c1}; centre = (min + max) * 0.5f in f32.
  *             ref >= 0: internal node index; ref < 0: leaf code
  *             0x80000000 | type << 28 | prim index (type: 0 sphere,
  *             1 triangle, 2 quad — scene_compiler.py:10-12).

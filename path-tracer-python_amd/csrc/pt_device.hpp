@@ -258,6 +258,10 @@ __device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, f
 
 __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 
+#ifndef PTMI_NODE_CENTRES
+#define PTMI_NODE_CENTRES 1
+#endif
+
 #ifndef PTMI_PUSH_BRANCHFREE
 #define PTMI_PUSH_BRANCHFREE 1
 #endif
@@ -318,7 +322,7 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
       continue;
     }
     // internal: kernels.py:698-740, both children at once
-    gf4* nd = nodes + 4 * ref;
+    gf4* nd = nodes + 5 * ref;  // 80-B node
     const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
     const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
     const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
@@ -332,9 +336,14 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
                              pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
     const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
     // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
+#if PTMI_NODE_CENTRES
+    const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
+    const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
+#else
     const pt_f2 half = pt_f2s(0.5f);
-    const pt_f2 dist = (((lox + hix) * half - ox) * dx + ((loy + hiy) * half - oy) * dy) +
-                       ((loz + hiz) * half - oz) * dz;
+    const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
+#endif
+    const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
     const bool ln = dist.x < dist.y;
     const int32_t r0 = __float_as_int(R.x), r1 = __float_as_int(R.y);
     const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;

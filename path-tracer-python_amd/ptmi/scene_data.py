@@ -173,6 +173,9 @@ def fixture_manifest():
 LEAF_FLAG = np.int64(0x80000000)
 
 
+NODE_FLOATS = 20  # 80-B internal node (include/ptmi.h)
+
+
 def leaf_code(prim_type, prim_idx):
     code = LEAF_FLAG | (np.int64(prim_type) << 28) | np.int64(prim_idx)
     return np.int32(np.int64(code) - (1 << 32))  # as signed int32 bits
@@ -181,7 +184,7 @@ def leaf_code(prim_type, prim_idx):
 @dataclass
 class DeviceLayout:
     """Host-side arrays in the device layout of include/ptmi.h."""
-    nodes: np.ndarray       # (n_inner, 16) f32
+    nodes: np.ndarray       # (n_inner, NODE_FLOATS) f32
     root_ref: int
     root_min: np.ndarray
     root_max: np.ndarray
@@ -263,13 +266,20 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
     cidx[internal] = np.arange(internal.shape[0])
     codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | pidx.astype(np.int64)) - (1 << 32)).astype(np.int32)
     refs = np.where(is_leaf, codes, cidx.astype(np.int32)).astype(np.int32)
-    nodes = np.zeros((internal.shape[0], 16), np.float32)
+    nodes = np.zeros((internal.shape[0], NODE_FLOATS), np.float32)
     if internal.size:  # children interleaved per component (include/ptmi.h)
         l, r = left[internal], right[internal]
         nodes[:, 0:12:2] = np.concatenate([bmin[l], bmax[l]], axis=1)
         nodes[:, 1:12:2] = np.concatenate([bmin[r], bmax[r]], axis=1)
         nodes[:, 12] = refs[l].view(np.float32)
         nodes[:, 13] = refs[r].view(np.float32)
+        # box centres (min + max) * 0.5 in f32 — the same rounding as the
+        # kernels' (kernels.py:707-710), so precomputing them changes nothing
+        cl = (bmin[l] + bmax[l]) * np.float32(0.5)
+        cr = (bmin[r] + bmax[r]) * np.float32(0.5)
+        nodes[:, 14], nodes[:, 15] = cl[:, 2], cr[:, 2]
+        nodes[:, 16], nodes[:, 17] = cl[:, 0], cr[:, 0]
+        nodes[:, 18], nodes[:, 19] = cl[:, 1], cr[:, 1]
     if n:
         root_ref = int(refs[0])
         root_min, root_max = bmin[0].copy(), bmax[0].copy()
