@@ -82,134 +82,169 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   // each wave renders an 8x8 pixel square (square footprints keep a wave's
   // camera rays coherent in the BVH); a 4-wave block covers 16x16.
   const int lane = tid & 63, wv = tid >> 6;
-  const int32_t lx = ((wv & 1) << 3) | (lane & 7);
-  const int32_t ly = ((wv >> 1) << 3) | (lane >> 3);
-  const int32_t px = fr.x0 + (int32_t)blockIdx.x * kMkTile + lx;
-  const int32_t lr = (int32_t)blockIdx.y * kMkTile + ly;
-  int32_t py = (lr < fr.n_rows) ? frame_row(fr, lr) : -1;
-  const bool valid = (px < fr.x0 + fr.w) && (py >= 0);
+  const int32_t sq_x = fr.x0 + (int32_t)blockIdx.x * kMkTile + ((wv & 1) << 3);  // the wave's square
+  const int32_t sq_y = (int32_t)blockIdx.y * kMkTile + ((wv >> 1) << 3);          // (local rows)
+  const size_t npix = (size_t)fr.w * (size_t)fr.n_rows;
+  const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
+  uint32_t n_seg = 0, n_med = 0, n_paths = 0;  // per-thread counts of one launch
+  PathState ps;
 
-  pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
-  float* ap = nullptr;
-  int32_t s = s_begin, s_end = s_begin + s_count;
-  if (STAGED) {  // this block's chunk of the call's samples
-    s = s_begin + (int32_t)blockIdx.z * chunk;
-    s_end = min(s + chunk, s_begin + s_count);
-    const size_t npix = (size_t)fr.w * (size_t)fr.n_rows;
-    ap = staging + 3 * ((size_t)(s - s_begin) * npix + (size_t)lr * (size_t)fr.w + (size_t)(px - fr.x0));
+  // Work of the wave. Direct mode: lane L owns pixel L of the square for all
+  // samples of the call (its accumulator lives in registers). Staged mode:
+  // the wave's (sample, pixel) items, sample-major, are handed out to lanes
+  // as their paths end (ballot + mbcnt, a wave-private counter: no atomics),
+  // so all 64 lanes stay busy until the wave's last few paths; any lane may
+  // render any item, because colours go to staging[sample][pixel].
+  int32_t s0 = s_begin, ns = s_count;
+  if (STAGED) {
+    s0 = s_begin + (int32_t)blockIdx.z * chunk;
+    ns = min(chunk, s_begin + s_count - s0);
   }
-  if (valid) {
+  const uint32_t total = 64u * (uint32_t)ns;
+  uint32_t next = 64u;  // wave-uniform: next unassigned item
+  uint32_t item = (uint32_t)lane;
+  int32_t px = 0, py = -1, lr = 0, s = s0;
+  float* ap = nullptr;
+  pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
+  bool live = false;
+  auto bind = [&](uint32_t k) -> bool {  // item -> pixel/sample; false if the pixel is outside the frame
+    const int32_t p = (int32_t)(k & 63u);
+    px = sq_x + (p & 7);
+    lr = sq_y + (p >> 3);
+    s = s0 + (int32_t)(k >> 6);
+    py = (lr < fr.n_rows && px < fr.x0 + fr.w) ? frame_row(fr, lr) : -1;
+    return py >= 0;
+  };
+  if (item < total && bind(item)) {
     if (!STAGED) {
       ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
       acc = pt_v3f(ap[0], ap[1], ap[2]);
     }
-  } else {
-    s = s_end;
+    start_path(fr, px, py, s, ps);
+    live = true;
   }
-  uint32_t n_seg = 0, n_med = 0, n_paths = 0;  // per-thread counts of one launch
-  const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
-  PathState ps;
-  if (s < s_end) start_path(fr, px, py, s, ps);
   __syncthreads();
 
-  while (s < s_end) {
-    const bool exit_mode = ps.mode == kModeMediumExit;
-    const float tmin = exit_mode ? ps.t_entry + 0.0001f : kTMin;  // kernels.py:418 / 1057
-    float t;
-    int32_t ref;
-    bool hit = traverse<STACK, kMkBlock>(sc, ps.o, ps.dir, tmin, kTMax, st, t, ref);
-    if (exit_mode) ++n_med; else ++n_seg;
+  for (;;) {
+    if (live) {
+      const bool exit_mode = ps.mode == kModeMediumExit;
+      const float tmin = exit_mode ? ps.t_entry + 0.0001f : kTMin;  // kernels.py:418 / 1057
+      float t;
+      int32_t ref;
+      bool hit = traverse<STACK, kMkBlock>(sc, ps.o, ps.dir, tmin, kTMax, st, t, ref);
+      if (exit_mode) ++n_med; else ++n_seg;
 
-    bool done = false, scattered = false, passthrough = false;
-    pt_v3 hp, sdir, att;
-    int32_t g = -1;
-    if (!exit_mode) {
-      if (!hit) {
-        ps.color = pt_add(ps.color, pt_mul(ps.thr, bg));  // kernels.py:1164-1168
-        done = true;
-      } else {
-        g = mat_index(sc, ref);
-        if ((mat_flags(sc, g) >> 8) & 1u) {  // medium boundary: exit search next iteration
-          ps.mode = kModeMediumExit;
-          ps.t_entry = t;
-          ps.ref_entry = ref;
-          continue;
-        }
-      }
-    } else {
-      g = mat_index(sc, ps.ref_entry);
-    }
-    if (g >= 0) {
-      const Mat m = load_mat(sc, g);
-      bool surface = !exit_mode;
-      int32_t sref = ref;
-      float st = t;
-      if (exit_mode) {
-        ps.mode = kModeTrace;
-        float t_exit;
-        pt_v3 mp;
-        // apply_constant_medium, kernels.py:421-448 (density m3.w)
-        if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
-          hp = mp;  // kernels.py:1082-1097
-          sdir = random_unit_vector(ps.rng);
-          att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
-          scattered = true;
-        } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
-          passthrough = true;
-          float rl = sqrtf(pt_dot(ps.dir, ps.dir));
-          float eps_t = 0.001f / rl;
-          ps.o = pt_add(ps.o, pt_scale(ps.dir, t_exit + eps_t));
-        } else {  // fallback: shade the boundary as a surface, kernels.py:1111-1119
-          surface = true;
-          sref = ps.ref_entry;
-          st = ps.t_entry;
-        }
-      }
-      if (surface) {  // kernels.py:1120-1128
-        hp = pt_add(ps.o, pt_scale(ps.dir, st));
-        pt_v3 n = hit_normal(sc, sref, hp, ps.dir);
-        ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
-        scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
-      }
-    }
-
-    if (!done) {
-      if (scattered) {  // kernels.py:1131-1157
-        ps.o = hp;
-        ps.dir = sdir;
-        ps.thr = pt_mul(ps.thr, att);
-        if (ps.depth + 1 >= fr.max_depth) {
+      bool done = false, scattered = false, passthrough = false, to_medium = false;
+      pt_v3 hp, sdir, att;
+      int32_t g = -1;
+      if (!exit_mode) {
+        if (!hit) {
+          ps.color = pt_add(ps.color, pt_mul(ps.thr, bg));  // kernels.py:1164-1168
           done = true;
         } else {
-          if (ps.depth + 1 >= kRRMinDepth) {
-            float sp = pt_minf(pt_maxf(pt_maxf(ps.thr.x, ps.thr.y), ps.thr.z), kRRMaxProb);
-            if (ps.rng.next() > sp) done = true;
-            else ps.thr = pt_divs(ps.thr, sp);
+          g = mat_index(sc, ref);
+          if ((mat_flags(sc, g) >> 8) & 1u) {  // medium boundary: exit search next iteration
+            ps.mode = kModeMediumExit;
+            ps.t_entry = t;
+            ps.ref_entry = ref;
+            to_medium = true;
           }
-          if (!done) ++ps.depth;
         }
-      } else if (passthrough) {
-        ++ps.depth;
-        if (ps.depth >= fr.max_depth) done = true;
       } else {
-        done = true;
+        g = mat_index(sc, ps.ref_entry);
+      }
+      if (g >= 0 && !to_medium) {
+        const Mat m = load_mat(sc, g);
+        bool surface = !exit_mode;
+        int32_t sref = ref;
+        float st = t;
+        if (exit_mode) {
+          ps.mode = kModeTrace;
+          float t_exit;
+          pt_v3 mp;
+          // apply_constant_medium, kernels.py:421-448 (density m3.w)
+          if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
+            hp = mp;  // kernels.py:1082-1097
+            sdir = random_unit_vector(ps.rng);
+            att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
+            scattered = true;
+          } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
+            passthrough = true;
+            float rl = sqrtf(pt_dot(ps.dir, ps.dir));
+            float eps_t = 0.001f / rl;
+            ps.o = pt_add(ps.o, pt_scale(ps.dir, t_exit + eps_t));
+          } else {  // fallback: shade the boundary as a surface, kernels.py:1111-1119
+            surface = true;
+            sref = ps.ref_entry;
+            st = ps.t_entry;
+          }
+        }
+        if (surface) {  // kernels.py:1120-1128
+          hp = pt_add(ps.o, pt_scale(ps.dir, st));
+          pt_v3 n = hit_normal(sc, sref, hp, ps.dir);
+          ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
+          scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
+        }
+      }
+
+      if (!done && !to_medium) {
+        if (scattered) {  // kernels.py:1131-1157
+          ps.o = hp;
+          ps.dir = sdir;
+          ps.thr = pt_mul(ps.thr, att);
+          if (ps.depth + 1 >= fr.max_depth) {
+            done = true;
+          } else {
+            if (ps.depth + 1 >= kRRMinDepth) {
+              float sp = pt_minf(pt_maxf(pt_maxf(ps.thr.x, ps.thr.y), ps.thr.z), kRRMaxProb);
+              if (ps.rng.next() > sp) done = true;
+              else ps.thr = pt_divs(ps.thr, sp);
+            }
+            if (!done) ++ps.depth;
+          }
+        } else if (passthrough) {
+          ++ps.depth;
+          if (ps.depth >= fr.max_depth) done = true;
+        } else {
+          done = true;
+        }
+      }
+      if (done) {
+        ++n_paths;
+        if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
+          float* o = staging + 3 * ((size_t)(s - s_begin) * npix + (size_t)lr * (size_t)fr.w + (size_t)(px - fr.x0));
+          o[0] = ps.color.x;
+          o[1] = ps.color.y;
+          o[2] = ps.color.z;
+          live = false;
+        } else {  // render_sample: accum += color (kernels.py:1187), next sample of the same pixel
+          acc = pt_add(acc, ps.color);
+          ++s;
+          live = s < s0 + ns;
+          if (live) start_path(fr, px, py, s, ps);
+        }
       }
     }
-    if (done) {
-      if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
-        ap[0] = ps.color.x;
-        ap[1] = ps.color.y;
-        ap[2] = ps.color.z;
-        ap += 3 * (size_t)fr.w * (size_t)fr.n_rows;
-      } else {
-        acc = pt_add(acc, ps.color);  // render_sample: accum += color (kernels.py:1187)
+    if (STAGED) {  // hand the wave's next items to the lanes without a path
+      const unsigned long long want = __ballot(!live);
+      if (want && next < total) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+        if (!live) {
+          item = next + rank;
+          if (item < total && bind(item)) {
+            start_path(fr, px, py, s, ps);
+            live = true;
+          }
+        }
+        next += (uint32_t)__popcll(want);
       }
-      ++n_paths;
-      ++s;
-      if (s < s_end) start_path(fr, px, py, s, ps);
+      if (__ballot(live) == 0ull && next >= total) break;
+    } else {
+      if (__ballot(live) == 0ull) break;
     }
   }
-  if (valid && !STAGED) {
+  if (!STAGED && ap) {
     ap[0] = acc.x;
     ap[1] = acc.y;
     ap[2] = acc.z;
