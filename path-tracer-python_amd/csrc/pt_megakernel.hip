@@ -320,6 +320,10 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
 #define PTMI_MK_TARGET_BLOCKS (16384 * 4 / PTMI_MK_BLOCK_WAVES)  // ~16 rounds of the chip's wave slots
 #endif
 
+#ifndef PTMI_MK_DIRECT_MIN_TILES
+#define PTMI_MK_DIRECT_MIN_TILES 0x7fffffff  // A/B: staged + item pool beat direct even at 4K (+3 %)
+#endif
+
 size_t mk_workspace_bytes(int32_t npix, int32_t batch) {
   if (npix <= 0 || batch <= 0) return 0;
   return (3 * sizeof(float) * (size_t)npix * (size_t)batch + 255) & ~(size_t)255;
@@ -348,7 +352,7 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
                             size_t ws_bytes, float* accum, int32_t s_begin, int32_t s_count,
                             unsigned long long* counters, hipStream_t stream) {
   const int64_t tiles = (int64_t)((fr.w + kMkTile - 1) / kMkTile) * ((fr.n_rows + kMkTile - 1) / kMkTile);
-  if (tiles >= PTMI_MK_TARGET_BLOCKS / 2 || s_count < 2)  // the tiles alone fill the chip: no staging
+  if (tiles >= PTMI_MK_DIRECT_MIN_TILES || s_count < 2)  // the tiles alone fill the chip: no staging
     return mk_render(sc, fr, stack_needed, accum, s_begin, s_count, counters, stream);
   const int32_t npix = fr.w * fr.n_rows;
   int32_t batch = s_count;
