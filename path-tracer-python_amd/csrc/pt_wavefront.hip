@@ -39,6 +39,9 @@
 namespace ptmi {
 
 constexpr int kShards = 8;
+#ifndef PTMI_WF_SQUARES
+#define PTMI_WF_SQUARES 1
+#endif
 #ifndef PTMI_WF_BLOCK
 #define PTMI_WF_BLOCK 256  // threads per block of the queue kernels
 #endif
@@ -60,6 +63,7 @@ struct WfBufs {
   int32_t capacity;   // queue slots (multiple of kShards * kWfBlock)
   int32_t medseg;     // slots per shard
   int32_t npix;       // pixels of the frame's pixel set
+  int32_t sq_tiles_x; // > 0: items walk 8x8 pixel squares (w, n_rows multiples of 8); 0: rows
   int32_t total;      // work items of the batch (= batch samples * npix)
   int32_t shard_len;  // items per shard: shard s owns [s*len, min((s+1)*len, total))
   int32_t s_begin;    // first sample of the batch
@@ -154,12 +158,25 @@ __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
 struct Item {
   int32_t srel, p, px, py;
 };
+// With square order, 64 consecutive items of a sample are one 8x8 pixel
+// square (regenerated lanes of a wave get neighbouring pixels, as in the
+// megakernel's waves); it.p is always the row-major pixel index (staging).
 __device__ __forceinline__ Item decode_item(const DevFrame& fr, const WfBufs& wb, uint32_t k) {
   Item it;
   it.srel = (int32_t)(k / (uint32_t)wb.npix);
-  it.p = (int32_t)(k - (uint32_t)it.srel * (uint32_t)wb.npix);
-  int32_t lr = it.p / fr.w;
-  it.px = fr.x0 + (it.p - lr * fr.w);
+  const int32_t q = (int32_t)(k - (uint32_t)it.srel * (uint32_t)wb.npix);
+  int32_t lr, lx;
+  if (wb.sq_tiles_x > 0) {
+    const int32_t t = q >> 6, r = q & 63;
+    const int32_t ty = t / wb.sq_tiles_x;
+    lx = (t - ty * wb.sq_tiles_x) * 8 + (r & 7);
+    lr = ty * 8 + (r >> 3);
+  } else {
+    lr = q / fr.w;
+    lx = q - lr * fr.w;
+  }
+  it.p = lr * fr.w + lx;
+  it.px = fr.x0 + lx;
   it.py = frame_row(fr, lr);
   return it;
 }
@@ -181,8 +198,9 @@ __device__ __forceinline__ Ray camera_ray(const DevFrame& fr, const WfBufs& wb, 
   return r;
 }
 
-__device__ __forceinline__ void stage(const WfBufs& wb, uint32_t k, pt_v3 c) {
-  float* p = wb.staging + 3 * (size_t)k;
+__device__ __forceinline__ void stage(const DevFrame& fr, const WfBufs& wb, uint32_t k, pt_v3 c) {
+  const Item it = decode_item(fr, wb, k);
+  float* p = wb.staging + 3 * ((size_t)it.srel * (size_t)wb.npix + (size_t)it.p);
   p[0] = c.x;
   p[1] = c.y;
   p[2] = c.z;
@@ -302,7 +320,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
       const int32_t ref = __float_as_int(h.y);
       const Ray ray = load_ray(q, i);
       if (ref == kMissRef) {
-        stage(wb, ray.item, pt_mul(ray.thr, bg));  // shade_miss_rays :1280
+        stage(fr, wb, ray.item, pt_mul(ray.thr, bg));  // shade_miss_rays :1280
         ended = true;
       } else {
         const int32_t g = mat_index(sc, ref);
@@ -320,7 +338,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
           go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
           if (!go) {
             ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
-            stage(wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
+            stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
                                                                                   : pt_v3f(0.0f, 0.0f, 0.0f));
           }
         }
@@ -403,7 +421,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, 
       }
       if (!go) {
         ended = true;
-        stage(wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
+        stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
                                                                               : pt_v3f(0.0f, 0.0f, 0.0f));
       }
     }
@@ -529,6 +547,11 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     wb.capacity = L.capacity;
     wb.medseg = L.medseg;
     wb.npix = npix;
+#if PTMI_WF_SQUARES
+    wb.sq_tiles_x = (fr.w % 8 == 0 && fr.n_rows % 8 == 0) ? fr.w / 8 : 0;
+#else
+    wb.sq_tiles_x = 0;
+#endif
     wb.total = npix * nb;
     wb.shard_len = (wb.total + kShards - 1) / kShards;
     wb.s_begin = s_begin + b0;
