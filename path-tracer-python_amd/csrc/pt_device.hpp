@@ -258,6 +258,17 @@ __device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, f
 
 __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 
+#ifndef PTMI_PROBE
+#define PTMI_PROBE 0
+#endif
+#if PTMI_PROBE
+__device__ unsigned long long g_probe[4];
+#endif
+
+#ifndef PTMI_UNIFORM_FETCH
+#define PTMI_UNIFORM_FETCH 0  // A/B on MI355X: -1.7 % (the v_mov of SGPR data costs more VALU than the texture path saves)
+#endif
+
 #ifndef PTMI_NODE_CENTRES
 #define PTMI_NODE_CENTRES 1
 #endif
@@ -321,31 +332,61 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
       }
       continue;
     }
-    // internal: kernels.py:698-740, both children at once
-    gf4* nd = nodes + 5 * ref;  // 80-B node
-    const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
-    const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
-    const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
-    const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
-    const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
-    const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
-    const float E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)),
-                             pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
-    const float X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
-    const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)),
-                             pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
-    const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
-    // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
-#if PTMI_NODE_CENTRES
-    const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
-    const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
-#else
-    const pt_f2 half = pt_f2s(0.5f);
-    const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
+#if PTMI_PROBE
+    {  // debug probe: node visits and wave-uniform node visits (lane counts)
+      const int32_t r0 = __builtin_amdgcn_readfirstlane(ref);
+      const bool uni = __ballot(ref != r0) == 0ull;
+      atomicAdd(&g_probe[0], 1ull);
+      if (uni) atomicAdd(&g_probe[1], 1ull);
+      const unsigned long long act = __ballot(true);
+      if (__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) == 0) {
+        atomicAdd(&g_probe[2], 1ull);  // wave-level node steps
+        atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
+      }
+    }
 #endif
-    const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
-    const bool ln = dist.x < dist.y;
-    const int32_t r0 = __float_as_int(R.x), r1 = __float_as_int(R.y);
+    // internal: kernels.py:698-740, both children at once
+    float E0, X0, E1, X1;
+    bool ln;
+    int32_t r0, r1;
+    auto expand = [&](const pt_f4 A, const pt_f4 B, const pt_f4 C, const pt_f4 R, const pt_f4 Cxy) {
+      const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
+      const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
+      const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
+      const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
+      const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
+      E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
+      X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
+      E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
+      X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
+      // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
+#if PTMI_NODE_CENTRES
+      const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
+#else
+      const pt_f2 half = pt_f2s(0.5f);
+      const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
+#endif
+      const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
+      ln = dist.x < dist.y;
+      r0 = __float_as_int(R.x);
+      r1 = __float_as_int(R.y);
+    };
+#if PTMI_UNIFORM_FETCH
+    // When every active lane expands the same node (about a third of the node
+    // visits: the top of the tree for a wave's coherent rays), fetch it with
+    // scalar loads through the scalar cache instead of 64 lanes' vector loads
+    // through the texture path (which runs ~80 % busy in this kernel).
+    const int32_t ru = __builtin_amdgcn_readfirstlane(ref);
+    if (__ballot(ref != ru) == 0ull) {
+      typedef const __attribute__((address_space(4))) pt_f4 cf4;
+      cf4* snd = (cf4*)sc.nodes + 5 * ru;
+      expand(snd[0], snd[1], snd[2], snd[3], PTMI_NODE_CENTRES ? snd[4] : snd[0]);
+    } else
+#endif
+    {
+      gf4* nd = nodes + 5 * ref;  // 80-B node
+      expand(nd[0], nd[1], nd[2], nd[3], PTMI_NODE_CENTRES ? nd[4] : nd[0]);
+    }
     const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
     const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
     const bool h0 = X0 >= E0, h1 = X1 >= E1;
