@@ -265,6 +265,10 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 __device__ unsigned long long g_probe[4];
 #endif
 
+#ifndef PTMI_POP_SKIP
+#define PTMI_POP_SKIP 0  // A/B on MI355X: skipping culled pops in an inner loop -11 %
+#endif
+
 #ifndef PTMI_UNIFORM_FETCH
 #define PTMI_UNIFORM_FETCH 0  // A/B on MI355X: -1.7 % (the v_mov of SGPR data costs more VALU than the texture path saves)
 #endif
@@ -319,10 +323,25 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
     }
   }
   while (sp > 0) {
+#if PTMI_POP_SKIP
+    // pop past culled entries in a tight loop (the same pop-time test, in the
+    // same order), so a lane reaches the leaf/node work with a live entry
+    // instead of spending a whole iteration of the wave on a culled one
+    uint2 ent;
+    bool live;
+    do {
+      --sp;
+      ent = st.slot0[sp * SB];
+      live = __uint_as_float(ent.y) <= closest;
+    } while (!live && sp > 0);
+    if (!live) break;
+    const int32_t ref = (int32_t)ent.x;
+#else
     --sp;
     const uint2 ent = st.slot0[sp * SB];
     const int32_t ref = (int32_t)ent.x;
     if (!(__uint_as_float(ent.y) <= closest)) continue;
+#endif
     if (ref < 0) {  // leaf: kernels.py:671-697
       float t;
       if (hit_leaf(sc, ref, o, d, tmin, closest, t) && t < closest) {
