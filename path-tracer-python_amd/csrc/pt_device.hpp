@@ -238,8 +238,10 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 //
 // A/B history on MI355X (all parity-identical): near-child shortcut with a
 // nested pop loop -17 %; top of stack in registers +0-2 % (mk) / -3 % (wf);
-// while-while -15 %; persistent lanes refilled per ray (wf) -7 %. This
-// push-both loop is the fastest measured.
+// while-while -15 %; persistent lanes refilled per ray (wf) -7 %; skipping
+// culled pops in an inner loop -11 %; scalar-cache fetch of wave-uniform
+// nodes -1.7 % (the SGPR->VGPR moves cost more VALU than the texture path
+// saves). Kept: packed pairs, precomputed centres, branch-free pushes.
 
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
@@ -265,31 +267,47 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 __device__ unsigned long long g_probe[4];
 #endif
 
-#ifndef PTMI_POP_SKIP
-#define PTMI_POP_SKIP 0  // A/B on MI355X: skipping culled pops in an inner loop -11 %
-#endif
-
-#ifndef PTMI_UNIFORM_FETCH
-#define PTMI_UNIFORM_FETCH 0  // A/B on MI355X: -1.7 % (the v_mov of SGPR data costs more VALU than the texture path saves)
-#endif
-
 #ifndef PTMI_NODE_CENTRES
 #define PTMI_NODE_CENTRES 1
-#endif
-
-#ifndef PTMI_PUSH_BRANCHFREE
-#define PTMI_PUSH_BRANCHFREE 1
 #endif
 
 #ifndef PTMI_NODES_VGPR
 #define PTMI_NODES_VGPR 1  // A/B on MI355X: +2 % megakernel
 #endif
 
+// In-flight traversal of one ray: begin (root test, push root) and one pop
+// of the loop per step, so a kernel can interleave steps of different rays'
+// traversals with other work; traverse() runs begin + steps to completion.
+struct Trav {
+  pt_v3 inv;
+  float tmin, closest;
+  int32_t best;  // leaf code of the closest hit; 0 = none (leaf codes are negative)
+  int32_t sp;
+  __device__ __forceinline__ bool any() const { return best != 0; }
+};
+
 template <int STACK, int SB = kBlock>
-__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
-                                         float& t_out, int32_t& ref_out) {
-  const pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
-                           fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+__device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack st, pt_v3 d, pt_v3 o, float tmin,
+                                           float tmax) {
+  tr.inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                  fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  tr.tmin = tmin;
+  tr.closest = tmax;
+  tr.best = 0;
+  tr.sp = 0;
+  if (sc.n_inner == 0 && sc.root_ref >= 0) return;  // empty scene
+  float E, X;
+  slab(o, tr.inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
+       tmin, E, X);
+  if (pt_minf(X, tr.closest) >= E) {
+    st.slot0[0] = make_uint2((uint32_t)sc.root_ref, __float_as_uint(E));
+    tr.sp = 1;
+  }
+}
+
+// One pop of the traversal loop; precondition tr.sp > 0.
+template <int STACK, int SB = kBlock>
+__device__ __forceinline__ void trav_step(const DevScene& sc, Trav& tr, Stack st, pt_v3 o, pt_v3 d) {
   // global address space: global_load, not flat_load (a laundered generic
   // pointer would otherwise lose it); clang vector type, no C++ copy ctor
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
@@ -301,139 +319,82 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
   // on the pop's critical path)
   asm volatile("" : "+v"(nodes));
 #endif
-  const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
-  const pt_f2 ix = pt_f2s(inv.x), iy = pt_f2s(inv.y), iz = pt_f2s(inv.z);
-  const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
-  float closest = tmax;
-  int32_t best = 0;
-  bool any = false;
-  int sp = 0;
-  if (sc.n_inner == 0 && sc.root_ref >= 0) {  // empty scene
-    t_out = tmax;
-    ref_out = 0;
-    return false;
-  }
-  {
-    float E, X;
-    slab(o, inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
-         tmin, E, X);
-    if (pt_minf(X, closest) >= E) {
-      st.slot0[0] = make_uint2((uint32_t)sc.root_ref, __float_as_uint(E));
-      sp = 1;
+  --tr.sp;
+  const uint2 ent = st.slot0[tr.sp * SB];
+  const int32_t ref = (int32_t)ent.x;
+  if (!(__uint_as_float(ent.y) <= tr.closest)) return;
+  if (ref < 0) {  // leaf: kernels.py:671-697
+    float t;
+    if (hit_leaf(sc, ref, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
+      tr.closest = t;
+      tr.best = ref;
     }
+    return;
   }
-  while (sp > 0) {
-#if PTMI_POP_SKIP
-    // pop past culled entries in a tight loop (the same pop-time test, in the
-    // same order), so a lane reaches the leaf/node work with a live entry
-    // instead of spending a whole iteration of the wave on a culled one
-    uint2 ent;
-    bool live;
-    do {
-      --sp;
-      ent = st.slot0[sp * SB];
-      live = __uint_as_float(ent.y) <= closest;
-    } while (!live && sp > 0);
-    if (!live) break;
-    const int32_t ref = (int32_t)ent.x;
-#else
-    --sp;
-    const uint2 ent = st.slot0[sp * SB];
-    const int32_t ref = (int32_t)ent.x;
-    if (!(__uint_as_float(ent.y) <= closest)) continue;
-#endif
-    if (ref < 0) {  // leaf: kernels.py:671-697
-      float t;
-      if (hit_leaf(sc, ref, o, d, tmin, closest, t) && t < closest) {
-        closest = t;
-        best = ref;
-        any = true;
-      }
-      continue;
-    }
 #if PTMI_PROBE
-    {  // debug probe: node visits and wave-uniform node visits (lane counts)
-      const int32_t r0 = __builtin_amdgcn_readfirstlane(ref);
-      const bool uni = __ballot(ref != r0) == 0ull;
-      atomicAdd(&g_probe[0], 1ull);
-      if (uni) atomicAdd(&g_probe[1], 1ull);
-      const unsigned long long act = __ballot(true);
-      if (__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) == 0) {
-        atomicAdd(&g_probe[2], 1ull);  // wave-level node steps
-        atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
-      }
-    }
-#endif
-    // internal: kernels.py:698-740, both children at once
-    float E0, X0, E1, X1;
-    bool ln;
-    int32_t r0, r1;
-    auto expand = [&](const pt_f4 A, const pt_f4 B, const pt_f4 C, const pt_f4 R, const pt_f4 Cxy) {
-      const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
-      const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
-      const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
-      const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
-      const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
-      E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
-      X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
-      E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
-      X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
-      // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
-#if PTMI_NODE_CENTRES
-      const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
-#else
-      const pt_f2 half = pt_f2s(0.5f);
-      const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
-#endif
-      const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
-      ln = dist.x < dist.y;
-      r0 = __float_as_int(R.x);
-      r1 = __float_as_int(R.y);
-    };
-#if PTMI_UNIFORM_FETCH
-    // When every active lane expands the same node (about a third of the node
-    // visits: the top of the tree for a wave's coherent rays), fetch it with
-    // scalar loads through the scalar cache instead of 64 lanes' vector loads
-    // through the texture path (which runs ~80 % busy in this kernel).
+  {  // debug probe: node visits and wave-uniform node visits (lane counts)
     const int32_t ru = __builtin_amdgcn_readfirstlane(ref);
-    if (__ballot(ref != ru) == 0ull) {
-      typedef const __attribute__((address_space(4))) pt_f4 cf4;
-      cf4* snd = (cf4*)sc.nodes + 5 * ru;
-      expand(snd[0], snd[1], snd[2], snd[3], PTMI_NODE_CENTRES ? snd[4] : snd[0]);
-    } else
-#endif
-    {
-      gf4* nd = nodes + 5 * ref;  // 80-B node
-      expand(nd[0], nd[1], nd[2], nd[3], PTMI_NODE_CENTRES ? nd[4] : nd[0]);
+    const bool uni = __ballot(ref != ru) == 0ull;
+    atomicAdd(&g_probe[0], 1ull);
+    if (uni) atomicAdd(&g_probe[1], 1ull);
+    const unsigned long long act = __ballot(true);
+    if (__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) == 0) {
+      atomicAdd(&g_probe[2], 1ull);  // wave-level node steps
+      atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
     }
-    const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
-    const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
-    const bool h0 = X0 >= E0, h1 = X1 >= E1;
-    const bool fh = ln ? h1 : h0, nh = ln ? h0 : h1;
-#if PTMI_PUSH_BRANCHFREE
-    // Far first, then near; each slot written unconditionally and kept only if
-    // its child is hit. No bound check: an internal node at depth d has at most
-    // d pending entries, so sp + 2 <= max_leaf_depth + 1 <= STACK always
-    // (STACK >= max_leaf_depth + 1 is enforced at dispatch) and the
-    // reference's overflow drop can never trigger.
-    st.slot0[sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
-    sp += fh ? 1 : 0;
-    st.slot0[sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
-    sp += nh ? 1 : 0;
-#else
-    if (fh && sp < STACK) {  // far first
-      st.slot0[sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
-      ++sp;
-    }
-    if (nh && sp < STACK) {
-      st.slot0[sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
-      ++sp;
-    }
-#endif
   }
-  t_out = closest;
-  ref_out = best;
-  return any;
+#endif
+  // internal: kernels.py:698-740, both children at once
+  const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
+  const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
+  const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
+  const float tmin = tr.tmin;
+  gf4* nd = nodes + 5 * ref;  // 80-B node
+  const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
+  const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
+  const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
+  const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
+  const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
+  const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
+  const float E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
+  const float X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
+  const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
+  const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
+  // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
+#if PTMI_NODE_CENTRES
+  const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
+  const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
+#else
+  const pt_f2 half = pt_f2s(0.5f);
+  const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
+#endif
+  const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
+  const bool ln = dist.x < dist.y;
+  const int32_t r0 = __float_as_int(R.x), r1 = __float_as_int(R.y);
+  const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
+  const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
+  const bool h0 = X0 >= E0, h1 = X1 >= E1;
+  const bool fh = ln ? h1 : h0, nh = ln ? h0 : h1;
+  // Far first, then near; each slot written unconditionally and kept only if
+  // its child is hit. No bound check: an internal node at depth d has at most
+  // d pending entries, so sp + 2 <= max_leaf_depth + 1 <= STACK always
+  // (STACK >= max_leaf_depth + 1 is enforced at dispatch) and the
+  // reference's overflow drop can never trigger.
+  st.slot0[tr.sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
+  tr.sp += fh ? 1 : 0;
+  st.slot0[tr.sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
+  tr.sp += nh ? 1 : 0;
+}
+
+template <int STACK, int SB = kBlock>
+__device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
+                                         float& t_out, int32_t& ref_out) {
+  Trav tr;
+  trav_begin<STACK, SB>(sc, tr, st, d, o, tmin, tmax);
+  while (tr.sp > 0) trav_step<STACK, SB>(sc, tr, st, o, d);
+  t_out = tr.closest;
+  ref_out = tr.best;
+  return tr.any();
 }
 
 // ---------------------------------------------------------------- textures

@@ -57,6 +57,10 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
   ps.ref_entry = 0;
 }
 
+#ifndef PTMI_MK_SHADE_AT
+#define PTMI_MK_SHADE_AT 8  // shade once at most this many lanes are still mid-traversal (A/B: 8 > 16 > 24 > 0)
+#endif
+
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -125,14 +129,37 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   }
   __syncthreads();
 
+  // Traversal of the current segment: begun when the segment starts and then
+  // advanced one pop at a time. The wave keeps stepping traversals while more
+  // than PTMI_MK_SHADE_AT lanes are still mid-traversal; then the lanes whose
+  // traversal has finished shade (and begin their next segment or take a new
+  // item) while the stragglers wait with their traversal state kept — instead
+  // of the whole wave idling until its longest traversal ends (node steps ran
+  // at ~35 % SIMD efficiency that way). 0 = wait for every lane.
+  Trav tr;
+  tr.sp = 0;
+  bool trav = false;  // a segment is in flight (traversal running or result pending)
+  auto begin_segment = [&]() {
+    const bool em = ps.mode == kModeMediumExit;
+    trav_begin<STACK, kMkBlock>(sc, tr, st, ps.dir, ps.o, em ? ps.t_entry + 0.0001f : kTMin, kTMax);  // :418/:1057
+    if (em) ++n_med; else ++n_seg;
+    trav = true;
+  };
+  if (live) begin_segment();
+
   for (;;) {
-    if (live) {
+    for (;;) {  // traversal steps
+      const int nbusy = __popcll(__ballot(trav && tr.sp > 0));
+      if (nbusy == 0) break;
+      if (nbusy <= PTMI_MK_SHADE_AT && __ballot(trav && tr.sp == 0) != 0ull) break;
+      if (trav && tr.sp > 0) trav_step<STACK, kMkBlock>(sc, tr, st, ps.o, ps.dir);
+    }
+    if (trav && tr.sp == 0) {  // segment traced: shade it
+      trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
-      const float tmin = exit_mode ? ps.t_entry + 0.0001f : kTMin;  // kernels.py:418 / 1057
-      float t;
-      int32_t ref;
-      bool hit = traverse<STACK, kMkBlock>(sc, ps.o, ps.dir, tmin, kTMax, st, t, ref);
-      if (exit_mode) ++n_med; else ++n_seg;
+      const bool hit = tr.any();
+      const float t = tr.closest;
+      const int32_t ref = tr.best;
 
       bool done = false, scattered = false, passthrough = false, to_medium = false;
       pt_v3 hp, sdir, att;
@@ -143,7 +170,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
           done = true;
         } else {
           g = mat_index(sc, ref);
-          if ((mat_flags(sc, g) >> 8) & 1u) {  // medium boundary: exit search next iteration
+          if ((mat_flags(sc, g) >> 8) & 1u) {  // medium boundary: exit search next segment
             ps.mode = kModeMediumExit;
             ps.t_entry = t;
             ps.ref_entry = ref;
@@ -212,7 +239,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
       if (done) {
         ++n_paths;
         if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
-          float* o = staging + 3 * ((size_t)(s - s_begin) * npix + (size_t)lr * (size_t)fr.w + (size_t)(px - fr.x0));
+          // slot of this lane's item (recomputed: pixel/sample need not stay live)
+          const int32_t ip = (int32_t)(item & 63u);
+          const size_t srel = (size_t)(s0 - s_begin) + (size_t)(item >> 6);
+          float* o = staging + 3 * (srel * npix + (size_t)(sq_y + (ip >> 3)) * (size_t)fr.w +
+                                    (size_t)(sq_x + (ip & 7) - fr.x0));
           o[0] = ps.color.x;
           o[1] = ps.color.y;
           o[2] = ps.color.z;
@@ -221,8 +252,13 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
           acc = pt_add(acc, ps.color);
           ++s;
           live = s < s0 + ns;
-          if (live) start_path(fr, px, py, s, ps);
+          if (live) {
+            start_path(fr, px, py, s, ps);
+            begin_segment();
+          }
         }
+      } else {
+        begin_segment();  // next segment of this path (or its medium exit search)
       }
     }
     if (STAGED) {  // hand the wave's next items to the lanes without a path
@@ -235,6 +271,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
           if (item < total && bind(item)) {
             start_path(fr, px, py, s, ps);
             live = true;
+            begin_segment();
           }
         }
         next += (uint32_t)__popcll(want);
