@@ -138,6 +138,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   // at ~35 % SIMD efficiency that way). 0 = wait for every lane.
   Trav tr;
   tr.sp = 0;
+  tr.pend = 0;
   bool trav = false;  // a segment is in flight (traversal running or result pending)
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
@@ -149,12 +150,12 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
 
   for (;;) {
     for (;;) {  // traversal steps
-      const int nbusy = __popcll(__ballot(trav && tr.sp > 0));
+      const int nbusy = __popcll(__ballot(trav && tr.busy()));
       if (nbusy == 0) break;
-      if (nbusy <= PTMI_MK_SHADE_AT && __ballot(trav && tr.sp == 0) != 0ull) break;
-      if (trav && tr.sp > 0) trav_step<STACK, kMkBlock>(sc, tr, st, ps.o, ps.dir);
+      if (nbusy <= PTMI_MK_SHADE_AT && __ballot(trav && !tr.busy()) != 0ull) break;
+      if (trav && tr.busy()) trav_step<STACK, kMkBlock>(sc, tr, st, ps.o, ps.dir);
     }
-    if (trav && tr.sp == 0) {  // segment traced: shade it
+    if (trav && !tr.busy()) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
       const bool hit = tr.any();
