@@ -264,7 +264,7 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 #define PTMI_PROBE 0
 #endif
 #if PTMI_PROBE
-__device__ unsigned long long g_probe[4];
+__device__ unsigned long long g_probe[8];
 #endif
 
 #ifndef PTMI_NODE_CENTRES
@@ -346,6 +346,11 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, Trav& tr, Stack st
   --tr.sp;
   const uint2 ent = st.slot0[tr.sp * SB];
   const int32_t ref = (int32_t)ent.x;
+#if PTMI_PROBE
+  atomicAdd(&g_probe[4], 1ull);                                                    // pops
+  if (!(__uint_as_float(ent.y) <= tr.closest)) atomicAdd(&g_probe[5], 1ull);       // culled pops
+  else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
+#endif
   if (!(__uint_as_float(ent.y) <= tr.closest)) return;
   if (ref < 0) {
 #if PTMI_LEAF_DEFER

@@ -415,9 +415,9 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
 #if PTMI_PROBE
 extern "C" int ptmi_probe_read(unsigned long long* out, int reset) {
   hipDeviceSynchronize();
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi::g_probe), 4 * sizeof(unsigned long long));
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi::g_probe), 8 * sizeof(unsigned long long));
   if (reset) {
-    unsigned long long z[4] = {0, 0, 0, 0};
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     hipMemcpyToSymbol(HIP_SYMBOL(ptmi::g_probe), z, sizeof(z));
   }
   return 0;

@@ -21,14 +21,16 @@ integ = device.Integrator(device.DeviceScene.from_arrays(sa))
 fr = device.make_frame(cam, bg, 50, 0, W, H)
 acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
 lib = _lib.load()
-out = (C.c_ulonglong * 4)()
+out = (C.c_ulonglong * 8)()
 lib.ptmi_probe_read(out, 1)
 integ.reset_counters()
 integ.render_mk(fr, acc, 0, spp)
 torch.cuda.synchronize()
 lib.ptmi_probe_read(out, 1)
 c = integ.read_counters()
-n, u, steps, lanes = list(out)
+n, u, steps, lanes, pops, culled, lsph, lother = list(out)
 print(json.dumps({'scene': scene, 'spp': spp, 'node_visits': n, 'uniform_visit_frac': u / max(1, n),
                   'simd_eff_node_steps': lanes / max(1, 64 * steps), 'node_visits_per_traversal':
-                  n / max(1, c['segments'] + c['medium']), **c}))
+                  n / max(1, c['segments'] + c['medium']), 'pops_per_traversal': pops / max(1, c['segments'] + c['medium']),
+                  'culled_frac': culled / max(1, pops), 'leaf_tests_per_traversal': (lsph + lother) / max(1, c['segments'] + c['medium']),
+                  'sphere_leaf_frac': lsph / max(1, lsph + lother), **c}))
