@@ -39,14 +39,18 @@
 namespace ptmi {
 
 constexpr int kShards = 8;
-#ifndef PTMI_WF_SQUARES
-#define PTMI_WF_SQUARES 1
+#ifndef PTMI_WF_CHUNK_SAMPLES
+#define PTMI_WF_CHUNK_SAMPLES 4  // samples per work chunk (one 8x8 pixel square each)
+#endif
+#ifndef PTMI_WF_TAIL
+#define PTMI_WF_TAIL 2  // a shard hands out single units once it has < TAIL chunks per group left
 #endif
 #ifndef PTMI_WF_BLOCK
 #define PTMI_WF_BLOCK 256  // threads per block of the queue kernels
 #endif
 constexpr int kWfBlock = PTMI_WF_BLOCK;
-constexpr uint32_t kDead = 0xffffffffu;  // item of an empty slot
+constexpr uint32_t kDead = 0xffffffffu;     // item of a retired slot
+constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (assigned in wf_intersect)
 
 struct Queue {
   float4* a;  // o.xyz, d.x
@@ -62,10 +66,14 @@ struct WfBufs {
   int32_t* ctl;       // kCtlWords counters, one per 256-B line (see ctl_*)
   int32_t capacity;   // queue slots (multiple of kShards * kWfBlock)
   int32_t medseg;     // slots per shard
+  int2* grp;          // per 64-slot group (one wave in wf_intersect): {next item, end} of its fetched units
   int32_t npix;       // pixels of the frame's pixel set
-  int32_t sq_tiles_x; // > 0: items walk 8x8 pixel squares (w, n_rows multiples of 8); 0: rows
-  int32_t total;      // work items of the batch (= batch samples * npix)
-  int32_t shard_len;  // items per shard: shard s owns [s*len, min((s+1)*len, total))
+  int32_t sq_x, nsq;  // 8x8 pixel squares covering the pixel set: per row, total
+  int32_t csamp;      // samples per chunk: a chunk is one square x csamp samples (64 * csamp items)
+  int32_t batch;      // samples of the batch
+  int32_t nunits;     // 64-item units of the batch (one square x one sample; csamp per chunk)
+  int32_t shard_len;  // units per shard (a multiple of csamp): shard s owns [s*len, min((s+1)*len, nunits))
+  int32_t shard_groups; // 64-slot groups drawing from each shard
   int32_t s_begin;    // first sample of the batch
 };
 
@@ -73,8 +81,8 @@ constexpr int32_t kMissRef = 0x7fffffff;
 
 // Device-scope atomics are performed per cache line at the memory side, so
 // counters sharing a line serialize as one: every counter gets its own
-// 256-B line. Lines 0-7: medium-queue count per shard; 8-15: next work item
-// per shard; 16: live slots (read by the host between chunks).
+// 256-B line. Lines 0-7: medium-queue count per shard; 8-15: next unit per
+// shard; 16: live slots (read by the host between iterations).
 constexpr int32_t kLine = 64;
 constexpr int32_t kCtlWords = 17 * kLine;
 __host__ __device__ __forceinline__ int32_t* ctl_medium(const WfBufs& wb, int32_t s) { return wb.ctl + s * kLine; }
@@ -83,11 +91,10 @@ __host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
-// Slot i is processed by block (i / kWfBlock) % grid, grid a multiple of kShards.
+// Slot i is processed by block (i / kWfBlock) % grid, grid a multiple of
+// kShards, so block b's slots draw chunks from shard b % kShards (blocks b and
+// b + 8 share an XCD). A 64-slot group is always one wave of wf_intersect.
 __device__ __forceinline__ int32_t slot_shard(int32_t i) { return (i / kWfBlock) % kShards; }
-__device__ __forceinline__ int32_t slot_rank(int32_t i) {  // index of slot i among its shard's slots
-  return ((i / kWfBlock) / kShards) * kWfBlock + (i % kWfBlock);
-}
 
 // Wave-aggregated counter increment: this lane's ticket (meaningful only if want).
 __device__ __forceinline__ int32_t wave_ticket(bool want, int32_t* counter) {
@@ -153,31 +160,29 @@ __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
   return r;
 }
 
-// Work item k -> (sample, image pixel): sample-major, pixels row-major over
-// the frame's pixel set.
+// Work items come in chunks of one 8x8 pixel square x csamp samples. Chunk c
+// is square c % nsq of sample block c / nsq (so early chunks cover every
+// square); item j of a chunk is pixel j % 64 of the square, sample j / 64 of
+// the block. Each 64-slot group works through one chunk at a time, so a
+// wave's rays come from one pixel square — the coherence the megakernel's
+// waves get from their 8x8 squares. Items outside the frame or past the
+// batch are skipped. it.p is the row-major pixel index (staging).
 struct Item {
   int32_t srel, p, px, py;
+  bool valid;
 };
-// With square order, 64 consecutive items of a sample are one 8x8 pixel
-// square (regenerated lanes of a wave get neighbouring pixels, as in the
-// megakernel's waves); it.p is always the row-major pixel index (staging).
 __device__ __forceinline__ Item decode_item(const DevFrame& fr, const WfBufs& wb, uint32_t k) {
   Item it;
-  it.srel = (int32_t)(k / (uint32_t)wb.npix);
-  const int32_t q = (int32_t)(k - (uint32_t)it.srel * (uint32_t)wb.npix);
-  int32_t lr, lx;
-  if (wb.sq_tiles_x > 0) {
-    const int32_t t = q >> 6, r = q & 63;
-    const int32_t ty = t / wb.sq_tiles_x;
-    lx = (t - ty * wb.sq_tiles_x) * 8 + (r & 7);
-    lr = ty * 8 + (r >> 3);
-  } else {
-    lr = q / fr.w;
-    lx = q - lr * fr.w;
-  }
+  const uint32_t per = 64u * (uint32_t)wb.csamp;
+  const uint32_t c = k / per, j = k - c * per;
+  const uint32_t blk = c / (uint32_t)wb.nsq, q = c - blk * (uint32_t)wb.nsq;
+  const int32_t qy = (int32_t)(q / (uint32_t)wb.sq_x), qx = (int32_t)q - qy * wb.sq_x;
+  const int32_t lx = qx * 8 + (int32_t)(j & 7u), lr = qy * 8 + (int32_t)((j >> 3) & 7u);
+  it.srel = (int32_t)blk * wb.csamp + (int32_t)(j >> 6);
+  it.valid = lx < fr.w && lr < fr.n_rows && it.srel < wb.batch;
   it.p = lr * fr.w + lx;
   it.px = fr.x0 + lx;
-  it.py = frame_row(fr, lr);
+  it.py = it.valid ? frame_row(fr, lr) : 0;
   return it;
 }
 
@@ -208,29 +213,89 @@ __device__ __forceinline__ void stage(const DevFrame& fr, const WfBufs& wb, uint
 
 __device__ __forceinline__ int32_t shard_end(const WfBufs& wb, int32_t s) {
   int64_t e = (int64_t)(s + 1) * wb.shard_len;
-  return e < wb.total ? (int32_t)e : wb.total;
+  return e < wb.nunits ? (int32_t)e : wb.nunits;
 }
 
-// Initial fill: the r-th slot of shard s takes item s*shard_len + r.
+// Next units for a group of shard `shard` (one lane calls it), stealing from
+// the other shards once its own range is spent: {first, end} unit, or
+// first = -1 when the batch is done. A whole chunk (csamp units of one
+// square) while the shard has plenty left; single units in its tail, so no
+// group is left with a long private queue while the others retire.
+__device__ __forceinline__ int2 fetch_units(const WfBufs& wb, int32_t shard) {
+  for (int32_t a = 0; a < kShards; ++a) {
+    const int32_t s = (shard + a) % kShards;
+    const int32_t e = shard_end(wb, s);
+    const int32_t cur = __hip_atomic_load(ctl_next(wb, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur >= e) continue;
+    const int32_t take = (e - cur) >= PTMI_WF_TAIL * wb.shard_groups * wb.csamp ? wb.csamp : 1;
+    const int32_t t = atomicAdd(ctl_next(wb, s), take);
+    if (t < e) return make_int2(t, t + take < e ? t + take : e);
+  }
+  return make_int2(-1, -1);
+}
+
+// Initial state: every slot waits for work; groups own no units yet; shard s
+// starts at its first unit.
 __global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb) {
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kWfBlock)) {
-    const int32_t s = slot_shard(i);
-    const int64_t k = (int64_t)s * wb.shard_len + slot_rank(i);
-    const bool live = slot_rank(i) < wb.shard_len && k < shard_end(wb, s);
-    if (live) store_ray(wb.q, i, camera_ray(fr, wb, (uint32_t)k));
-    else kill_slot(wb.q, i);
-    wave_add(live, ctl_live(wb), 1);
+    reinterpret_cast<uint32_t*>(wb.q.c + i)[1] = kPending;
+    if ((i & 63) == 0) wb.grp[i >> 6] = make_int2(0, 0);
   }
   if (blockIdx.x < kShards && threadIdx.x == 0) {
     const int32_t s = (int32_t)blockIdx.x;
-    const int64_t k = (int64_t)s * wb.shard_len + wb.medseg;
-    *ctl_next(wb, s) = (int32_t)(k < shard_end(wb, s) ? k : shard_end(wb, s));
+    *ctl_next(wb, s) = min(s * wb.shard_len, wb.nunits);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctl_live(wb) = wb.capacity;
+}
+
+// Hand the group's (this wave's) next items to its slots waiting for work,
+// taking a new chunk when the current one runs out; slots that find no work
+// retire. Wave-uniform: called by all 64 lanes of the group.
+__device__ __forceinline__ void assign_work(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& item) {
+  const bool pending = item == kPending;
+  const unsigned long long pm = __ballot(pending);
+  if (pm == 0ull) return;
+  const int32_t g = i >> 6;
+  const uint32_t n = (uint32_t)__popcll(pm);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+  const int2 gs = wb.grp[g];
+  uint32_t nxt = (uint32_t)gs.x, end = (uint32_t)gs.y;
+  const uint32_t avail = end - nxt;
+  uint32_t my = kDead;
+  if (rank < avail) my = nxt + rank;
+  if (n > avail) {  // the group needs new units (>= 64 items: one fetch is enough)
+    int2 u = make_int2(0, 0);
+    const int32_t leader = __ffsll((long long)pm) - 1;
+    if (lane_id() == leader) u = fetch_units(wb, slot_shard(i));
+    u.x = __shfl(u.x, leader);
+    u.y = __shfl(u.y, leader);
+    if (u.x >= 0) {
+      const uint32_t cb = 64u * (uint32_t)u.x;
+      if (rank >= avail) my = cb + (rank - avail);
+      nxt = cb + (n - avail);
+      end = 64u * (uint32_t)u.y;
+    } else {
+      nxt = end;
+    }
+  } else {
+    nxt += n;
+  }
+  if (lane_id() == 0) wb.grp[g] = make_int2((int32_t)nxt, (int32_t)end);
+  if (pending) {
+    if (my == kDead) {
+      kill_slot(wb.q, i);
+      item = kDead;
+    } else if (decode_item(fr, wb, my).valid) {
+      store_ray(wb.q, i, camera_ray(fr, wb, my));
+      item = my;
+    }  // an item outside the frame / batch: the slot stays pending
+  }
+  wave_add(pending && my == kDead, ctl_live(wb), -1);
 }
 
 // intersect_rays, kernels.py:1242-1263.
 template <int STACK>
-__global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb,
                                                        unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   const int tid = threadIdx.x;
@@ -240,7 +305,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, WfBufs wb,
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_live = 0;
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + tid); i < wb.capacity; i += stride) {
-    if (slot_item(q, i) == kDead) continue;
+    uint32_t item = slot_item(q, i);
+    assign_work(fr, wb, i, item);  // generate_camera_rays (kernels.py:1219-1239) for slots that need work
+    if (item >= kPending) continue;
     ++n_live;
     float4 a = q.a[i], b = q.b[i];
     pt_v3 o = pt_v3f(a.x, a.y, a.z), d = pt_v3f(a.w, b.x, b.y);
@@ -277,27 +344,11 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
 }
 
 // Per-lane tail of both shading kernels: keep a continuing ray in its slot,
-// or give an ended path's slot the next work item of its shard (stealing from
-// the other shards once its own range is spent), or retire the slot.
-__device__ __forceinline__ void finish_lane(const DevFrame& fr, const WfBufs& wb, int32_t i, int32_t shard,
-                                            bool ended, bool go, const Ray& cont) {
+// or mark the slot of an ended path as waiting for work (the next
+// wf_intersect hands it the next item of its group's chunk).
+__device__ __forceinline__ void finish_lane(const WfBufs& wb, int32_t i, bool ended, bool go, const Ray& cont) {
   if (go) store_ray(wb.q, i, cont);
-  bool need = ended;
-  int32_t k = -1;
-  for (int32_t a = 0; a < kShards; ++a) {  // wave-uniform loop (ballot inside)
-    if (__ballot(need) == 0ull) break;
-    const int32_t s = (shard + a) % kShards;
-    const int32_t t = wave_ticket(need, ctl_next(wb, s));
-    if (need && t < shard_end(wb, s)) {
-      k = t;
-      need = false;
-    }
-  }
-  if (ended) {
-    if (k >= 0) store_ray(wb.q, i, camera_ray(fr, wb, (uint32_t)k));
-    else kill_slot(wb.q, i);
-  }
-  wave_add(ended && k < 0, ctl_live(wb), -1);
+  if (ended) reinterpret_cast<uint32_t*>(wb.q.c + i)[1] = kPending;
 }
 
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
@@ -314,7 +365,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
     const int32_t i = base + (int32_t)threadIdx.x;
     bool to_medium = false, ended = false, go = false;
     Ray cont;
-    const bool live = i < wb.capacity && slot_item(q, i) != kDead;
+    const bool live = i < wb.capacity && slot_item(q, i) < kPending;
     if (live) {
       const float2 h = wb.hit[i];
       const int32_t ref = __float_as_int(h.y);
@@ -346,7 +397,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
     }
     const int32_t mslot = wave_ticket(to_medium, ctl_medium(wb, shard));
     if (to_medium) wb.medq[shard * wb.medseg + mslot] = i;
-    finish_lane(fr, wb, i, shard, ended, go, cont);
+    finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
   if (counters) block_flush(n_ended, &tally, counters + 2);
@@ -427,7 +478,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, 
     }
     // refill from the block's shard: the segment shard varies across a wave,
     // and the ticket counter must be wave-uniform
-    finish_lane(fr, wb, i, (int32_t)(blockIdx.x % kShards), ended, go, cont);
+    finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
   if (counters) block_flush(n_ended, lds_stack, counters + 2);
@@ -443,7 +494,7 @@ constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
 struct Layout {
   int32_t capacity, medseg;
-  size_t q, hit, medq, staging, ctl, total;
+  size_t q, hit, medq, grp, staging, ctl, total;
 };
 
 Layout layout(int32_t npix, int32_t batch) {
@@ -458,7 +509,8 @@ Layout layout(int32_t npix, int32_t batch) {
   L.q = 0;
   L.hit = L.q + 3 * sizeof(float4) * c;
   L.medq = L.hit + sizeof(float2) * c;
-  L.staging = (L.medq + sizeof(int32_t) * c + 15) & ~(size_t)15;
+  L.grp = (L.medq + sizeof(int32_t) * c + 15) & ~(size_t)15;
+  L.staging = (L.grp + sizeof(int2) * (c / 64) + 15) & ~(size_t)15;
   L.ctl = (L.staging + 3 * sizeof(float) * (size_t)items + 255) & ~(size_t)255;
   L.total = L.ctl + kCtlWords * sizeof(int32_t);
   return L;
@@ -487,14 +539,14 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, fl
   prof_end(kProfWfGenerate, stream);
   // Each item needs at most max_depth waves and every iteration advances every
   // live ray by one wave, so total * max_depth iterations always drain the pool.
-  const int64_t max_iters = (int64_t)wb.total * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 1;
+  const int64_t max_iters = (int64_t)wb.nunits * 64 * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 2;
   int64_t it = 0;
   const int32_t chunk = 8;
   while (it < max_iters) {
     int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
       prof_begin(kProfWfIntersect, stream);
-      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kWfBlock), 0, stream, sc, wb, counters);
+      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
       prof_end(kProfWfIntersect, stream);
       prof_begin(kProfWfShade, stream);
       hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
@@ -542,18 +594,19 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     wb.q.c = (float4*)(p + L.q + 2 * sizeof(float4) * c);
     wb.hit = (float2*)(p + L.hit);
     wb.medq = (int32_t*)(p + L.medq);
+    wb.grp = (int2*)(p + L.grp);
     wb.staging = (float*)(p + L.staging);
     wb.ctl = (int32_t*)(p + L.ctl);
     wb.capacity = L.capacity;
     wb.medseg = L.medseg;
     wb.npix = npix;
-#if PTMI_WF_SQUARES
-    wb.sq_tiles_x = (fr.w % 8 == 0 && fr.n_rows % 8 == 0) ? fr.w / 8 : 0;
-#else
-    wb.sq_tiles_x = 0;
-#endif
-    wb.total = npix * nb;
-    wb.shard_len = (wb.total + kShards - 1) / kShards;
+    wb.sq_x = (fr.w + 7) / 8;
+    wb.nsq = wb.sq_x * ((fr.n_rows + 7) / 8);
+    wb.batch = nb;
+    wb.csamp = nb < PTMI_WF_CHUNK_SAMPLES ? nb : PTMI_WF_CHUNK_SAMPLES;
+    wb.nunits = wb.nsq * ((nb + wb.csamp - 1) / wb.csamp) * wb.csamp;
+    wb.shard_len = (wb.nunits / wb.csamp + kShards - 1) / kShards * wb.csamp;
+    wb.shard_groups = L.capacity / 64 / kShards;
     wb.s_begin = s_begin + b0;
     hipError_t e;
     if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wb, accum, nb, counters, stream);
