@@ -354,6 +354,9 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
 }
 
 // ---------------------------------------------------------------- staged
+#ifndef PTMI_MK_STAGED_MIN_STACK
+#define PTMI_MK_STAGED_MIN_STACK 0  // staged: STACK 16 scenes use the 20-slot kernel (the 16-slot one spills 12 B/lane; same 4 waves/SIMD): +0.8 % C2
+#endif
 #ifndef PTMI_MK_TARGET_BLOCKS
 #define PTMI_MK_TARGET_BLOCKS (16384 * 4 / PTMI_MK_BLOCK_WAVES)  // ~16 rounds of the chip's wave slots
 #endif
@@ -400,7 +403,7 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
     const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
     float* st = (float*)ws;
     hipError_t e;
-    if (stack_needed <= 16) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 20) e = launch_mk_staged<20>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 24) e = launch_mk_staged<24>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 32) e = launch_mk_staged<32>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
