@@ -17,14 +17,20 @@
 //     after a few bounces its queues are nearly empty. Here the (sample,
 //     pixel) pairs of a batch are work items: a queue slot keeps its ray in
 //     place from bounce to bounce (no append, no swap copy: kernels.py:
-//     1402-1418 removed) and, when the path ends, takes the camera ray of the
-//     next work item — so every launch works on a full queue until the batch
-//     runs out. Work-item counters and the medium-queue counters are sharded
-//     8 ways by slot block (blocks b and b+8 share an XCD), with one
-//     wave-aggregated atomic per wave, because a single device-wide counter
-//     saturates near 88 returning atomics/us on MI355X (MI355X_MICROARCH.md,
-//     "dequeue") and was measured at 97 % wait cycles in the shade kernel.
-//     Each ray carries its own wave count and is dropped at max_depth waves,
+//     1402-1418 removed) and, when the path ends, waits for the next
+//     wf_intersect, which hands it the camera ray of the next work item — so
+//     every launch works on a full queue until the batch runs out.
+//   * Work is handed out per 64-slot group (one wave): a group draws 64-item
+//     units (one 8x8 pixel square x one sample) in chunks of a few samples of
+//     the same square, so a wave's rays stay coherent. Unit counters are
+//     sharded 8 ways by slot block (blocks b and b+8 share an XCD), one
+//     atomic per chunk, each counter on its own 256-B line, because a single
+//     device-wide counter saturates near 88 returning atomics/us on MI355X
+//     (MI355X_MICROARCH.md, "dequeue") and was measured at 97 % wait cycles.
+//   * PIPES: the queue is split into 4 independent parts, each looping
+//     intersect -> shade -> medium on its own stream, so the drain at the end
+//     of one pipe's launch is filled by another's (+21 % over one pipe).
+//   * Each ray carries its own wave count and is dropped at max_depth waves,
 //     exactly the reference's per-path budget (Q14, incl. passthrough Q11).
 //   * A path adds at most one colour to its pixel, when it ends (a miss, or an
 //     emissive hit, which never scatters: kernels.py:1266-1280, 1365-1375,
@@ -63,7 +69,8 @@ struct WfBufs {
   float2* hit;        // t, ref (bits); ref kMissRef = miss
   int32_t* medq;      // kShards segments of medseg slot indices
   float* staging;     // [batch][npix][3] path colours
-  int32_t* ctl;       // kCtlWords counters, one per 256-B line (see ctl_*)
+  int32_t* ctl;       // this pipe's counters, one per 256-B line (see ctl_*)
+  int32_t* next;      // next-unit counters shared by the pipes, one per 256-B line
   int32_t capacity;   // queue slots (multiple of kShards * kWfBlock)
   int32_t medseg;     // slots per shard
   int2* grp;          // per 64-slot group (one wave in wf_intersect): {next item, end} of its fetched units
@@ -79,15 +86,25 @@ struct WfBufs {
 
 constexpr int32_t kMissRef = 0x7fffffff;
 
+// Pipes: the queue is split into PTMI_WF_PIPES independent halves, each
+// driven through its own intersect/shade/medium loop on its own stream, so
+// one pipe's kernels fill the drain at the end of the other's. They share the
+// work pool (next-unit counters) and the staging buffer.
+#ifndef PTMI_WF_PIPES
+#define PTMI_WF_PIPES 4  // A/B on MI355X: 1 -> 2 pipes +15 % (C3), 2 -> 4 +5 %
+#endif
+constexpr int32_t kPipes = PTMI_WF_PIPES;
+
 // Device-scope atomics are performed per cache line at the memory side, so
 // counters sharing a line serialize as one: every counter gets its own
-// 256-B line. Lines 0-7: medium-queue count per shard; 8-15: next unit per
-// shard; 16: live slots (read by the host between iterations).
+// 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 9 lines:
+// medium-queue count per shard, live slots (read by the host).
 constexpr int32_t kLine = 64;
-constexpr int32_t kCtlWords = 17 * kLine;
+constexpr int32_t kPipeLines = 9;
+constexpr int32_t kCtlWords = (8 + kPipeLines * kPipes) * kLine;
 __host__ __device__ __forceinline__ int32_t* ctl_medium(const WfBufs& wb, int32_t s) { return wb.ctl + s * kLine; }
-__host__ __device__ __forceinline__ int32_t* ctl_next(const WfBufs& wb, int32_t s) { return wb.ctl + (8 + s) * kLine; }
-__host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl + 16 * kLine; }
+__host__ __device__ __forceinline__ int32_t* ctl_next(const WfBufs& wb, int32_t s) { return wb.next + s * kLine; }
+__host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl + 8 * kLine; }
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -236,12 +253,12 @@ __device__ __forceinline__ int2 fetch_units(const WfBufs& wb, int32_t shard) {
 
 // Initial state: every slot waits for work; groups own no units yet; shard s
 // starts at its first unit.
-__global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb) {
+__global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb, int32_t init_next) {
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kWfBlock)) {
     reinterpret_cast<uint32_t*>(wb.q.c + i)[1] = kPending;
     if ((i & 63) == 0) wb.grp[i >> 6] = make_int2(0, 0);
   }
-  if (blockIdx.x < kShards && threadIdx.x == 0) {
+  if (init_next && blockIdx.x < kShards && threadIdx.x == 0) {
     const int32_t s = (int32_t)blockIdx.x;
     *ctl_next(wb, s) = min(s * wb.shard_len, wb.nunits);
   }
@@ -476,8 +493,6 @@ __global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, 
                                                                               : pt_v3f(0.0f, 0.0f, 0.0f));
       }
     }
-    // refill from the block's shard: the segment shard varies across a wave,
-    // and the ticket counter must be wave-uniform
     finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
@@ -485,9 +500,33 @@ __global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, 
 }
 
 namespace {
-int32_t* g_pinned_live = nullptr;  // host-pinned readback slot for the live-slot count
+int32_t* g_pinned_live = nullptr;  // host-pinned readback slots for the pipes' live-slot counts
+
+// Library-owned streams and fork/join events for pipes 1.., per device.
+struct PipeStreams {
+  hipStream_t s[kPipes] = {};
+  hipEvent_t fork = nullptr, join[kPipes] = {};
+  bool ok = false;
+};
+PipeStreams g_pipes[64];
+
+hipError_t pipe_streams(PipeStreams*& ps) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  ps = &g_pipes[dev];
+  if (ps->ok) return hipSuccess;
+  e = hipEventCreateWithFlags(&ps->fork, hipEventDisableTiming);
+  for (int p = 1; p < kPipes && e == hipSuccess; ++p) {
+    e = hipStreamCreateWithFlags(&ps->s[p], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ps->join[p], hipEventDisableTiming);
+  }
+  ps->ok = e == hipSuccess;
+  return e;
+}
 #ifndef PTMI_WF_CAPACITY_LOG2
-#define PTMI_WF_CAPACITY_LOG2 20
+#define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
 #endif
 constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
 constexpr int32_t kSlotQuantum = kShards * kWfBlock;
@@ -502,9 +541,9 @@ Layout layout(int32_t npix, int32_t batch) {
   int64_t items = (int64_t)npix * batch;
   int64_t cap = npix > kMaxCapacity ? npix : kMaxCapacity;
   if (items < cap) cap = items;
-  cap = (cap + kSlotQuantum - 1) / kSlotQuantum * kSlotQuantum;
-  L.capacity = (int32_t)cap;
-  L.medseg = (int32_t)(cap / kShards);
+  cap = (cap + kPipes * kSlotQuantum - 1) / (kPipes * kSlotQuantum) * (kPipes * kSlotQuantum);
+  L.capacity = (int32_t)cap;  // all pipes; each pipe has capacity / kPipes slots
+  L.medseg = (int32_t)(cap / kPipes / kShards);
   size_t c = (size_t)cap;
   L.q = 0;
   L.hit = L.q + 3 * sizeof(float4) * c;
@@ -518,53 +557,86 @@ Layout layout(int32_t npix, int32_t batch) {
 }  // namespace
 
 #ifndef PTMI_WF_MAX_BLOCKS
-#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // multiple of kShards
+#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together
 #endif
-static_assert(PTMI_WF_MAX_BLOCKS % kShards == 0, "grid must be a multiple of the shard count");
+static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must be a multiple of the shard count");
 
+// One batch: generate on the caller's stream, fork the pipes, run each pipe's
+// intersect -> shade -> medium loop on its own stream until its slots have all
+// retired, join, resolve.
 template <int STACK>
-static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, WfBufs wb, float* accum, int32_t batch,
-                           unsigned long long* counters, hipStream_t stream) {
+static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs* wbs, float* accum, int32_t batch,
+                           unsigned long long* counters, hipStream_t stream, const PipeStreams& ps) {
 #ifdef PTMI_WF_NOCOUNT
   counters = nullptr;  // A/B only: prices the statistics atomics
 #endif
-  // grid = multiple of kShards and of the slot quantum, so slot i always maps
-  // to block (i / kWfBlock) % grid with shard (i / kWfBlock) % kShards
-  int64_t blocks = wb.capacity / kWfBlock;
-  if (blocks > PTMI_WF_MAX_BLOCKS) blocks = PTMI_WF_MAX_BLOCKS;
+  // a pipe's grid = multiple of kShards and of the slot quantum, so its slot i
+  // always maps to block (i / kWfBlock) % grid with shard (i / kWfBlock) % kShards
+  int64_t blocks = wbs[0].capacity / kWfBlock;
+  if (blocks > PTMI_WF_MAX_BLOCKS / kPipes) blocks = PTMI_WF_MAX_BLOCKS / kPipes;
   const unsigned g = (unsigned)blocks;
-  (void)hipMemsetAsync(wb.ctl, 0, kCtlWords * sizeof(int32_t), stream);
-  prof_begin(kProfWfGenerate, stream);
-  hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kWfBlock), 0, stream, fr, wb);
-  prof_end(kProfWfGenerate, stream);
+  (void)hipMemsetAsync(wbs[0].next, 0, kCtlWords * sizeof(int32_t), stream);
+  for (int p = 0; p < kPipes; ++p) {
+    prof_begin(kProfWfGenerate, stream);
+    hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kWfBlock), 0, stream, fr, wbs[p], (int32_t)(p == 0));
+    prof_end(kProfWfGenerate, stream);
+  }
+  hipStream_t st[kPipes];
+  st[0] = stream;
+  for (int p = 1; p < kPipes; ++p) st[p] = ps.s[p];
+  if (kPipes > 1) {
+    hipError_t e = hipEventRecord(ps.fork, stream);
+    for (int p = 1; p < kPipes && e == hipSuccess; ++p) e = hipStreamWaitEvent(st[p], ps.fork, 0);
+    if (e != hipSuccess) return e;
+  }
   // Each item needs at most max_depth waves and every iteration advances every
-  // live ray by one wave, so total * max_depth iterations always drain the pool.
-  const int64_t max_iters = (int64_t)wb.nunits * 64 * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 2;
+  // live ray by one wave (or hands a waiting slot an item), so this many
+  // iterations always drain a pipe.
+  const int64_t max_iters = (int64_t)wbs[0].nunits * 64 * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 2;
+  bool live[kPipes];
+  for (int p = 0; p < kPipes; ++p) live[p] = true;
   int64_t it = 0;
-  const int32_t chunk = 8;
+  const int32_t chunk = 8;  // iterations between live-count readbacks
+  hipError_t err = hipSuccess;
   while (it < max_iters) {
-    int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
+    const int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
-      prof_begin(kProfWfIntersect, stream);
-      hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
-      prof_end(kProfWfIntersect, stream);
-      prof_begin(kProfWfShade, stream);
-      hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
-      prof_end(kProfWfShade, stream);
-      prof_begin(kProfWfMedium, stream);
-      hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kWfBlock), 0, stream, sc, fr, wb, counters);
-      prof_end(kProfWfMedium, stream);
+      for (int p = 0; p < kPipes; ++p) {
+        if (!live[p]) continue;
+        const WfBufs& wb = wbs[p];
+        prof_begin(kProfWfIntersect, st[p]);
+        hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        prof_end(kProfWfIntersect, st[p]);
+        prof_begin(kProfWfShade, st[p]);
+        hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        prof_end(kProfWfShade, st[p]);
+        prof_begin(kProfWfMedium, st[p]);
+        hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        prof_end(kProfWfMedium, st[p]);
+      }
     }
     it += n;
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(g_pinned_live, ctl_live(wb), sizeof(int32_t), hipMemcpyDeviceToHost, stream);
-    if (e != hipSuccess) return e;
-    e = hipStreamSynchronize(stream);
-    if (e != hipSuccess) return e;
-    if (*g_pinned_live == 0) break;
+    err = hipGetLastError();
+    for (int p = 0; p < kPipes && err == hipSuccess; ++p)
+      if (live[p])
+        err = hipMemcpyAsync(g_pinned_live + p, ctl_live(wbs[p]), sizeof(int32_t), hipMemcpyDeviceToHost, st[p]);
+    for (int p = 0; p < kPipes && err == hipSuccess; ++p)
+      if (live[p]) err = hipStreamSynchronize(st[p]);
+    if (err != hipSuccess) break;
+    bool any = false;
+    for (int p = 0; p < kPipes; ++p) {
+      live[p] = live[p] && g_pinned_live[p] != 0;
+      any = any || live[p];
+    }
+    if (!any) break;
   }
-  return launch_stage_resolve(fr, wb.staging, wb.npix, batch, accum, kProfWfResolve, stream);
+  for (int p = 1; p < kPipes; ++p) {  // join (also on error: the caller's stream must not run ahead)
+    hipError_t e = hipEventRecord(ps.join[p], st[p]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, ps.join[p], 0);
+    if (err == hipSuccess) err = e;
+  }
+  if (err != hipSuccess) return err;
+  return launch_stage_resolve(fr, wbs[0].staging, wbs[0].npix, batch, accum, kProfWfResolve, stream);
 }
 
 size_t wf_workspace_bytes(int32_t npix, int32_t batch) {
@@ -580,40 +652,51 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
   while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
   if (layout(npix, batch).total > ws_bytes) return hipErrorInvalidValue;
   if (!g_pinned_live) {
-    hipError_t e = hipHostMalloc((void**)&g_pinned_live, sizeof(int32_t), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)&g_pinned_live, kPipes * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) return e;
+  }
+  PipeStreams* ps = nullptr;
+  if (kPipes > 1) {
+    hipError_t e = pipe_streams(ps);
+    if (e != hipSuccess) return e;
+  } else {
+    ps = &g_pipes[0];
   }
   for (int32_t b0 = 0; b0 < s_count; b0 += batch) {
     const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
     const Layout L = layout(npix, nb);
-    char* p = (char*)ws;
-    WfBufs wb;
-    size_t c = (size_t)L.capacity;
-    wb.q.a = (float4*)(p + L.q);
-    wb.q.b = (float4*)(p + L.q + sizeof(float4) * c);
-    wb.q.c = (float4*)(p + L.q + 2 * sizeof(float4) * c);
-    wb.hit = (float2*)(p + L.hit);
-    wb.medq = (int32_t*)(p + L.medq);
-    wb.grp = (int2*)(p + L.grp);
-    wb.staging = (float*)(p + L.staging);
-    wb.ctl = (int32_t*)(p + L.ctl);
-    wb.capacity = L.capacity;
-    wb.medseg = L.medseg;
-    wb.npix = npix;
-    wb.sq_x = (fr.w + 7) / 8;
-    wb.nsq = wb.sq_x * ((fr.n_rows + 7) / 8);
-    wb.batch = nb;
-    wb.csamp = nb < PTMI_WF_CHUNK_SAMPLES ? nb : PTMI_WF_CHUNK_SAMPLES;
-    wb.nunits = wb.nsq * ((nb + wb.csamp - 1) / wb.csamp) * wb.csamp;
-    wb.shard_len = (wb.nunits / wb.csamp + kShards - 1) / kShards * wb.csamp;
-    wb.shard_groups = L.capacity / 64 / kShards;
-    wb.s_begin = s_begin + b0;
+    char* base = (char*)ws;
+    const size_t c = (size_t)L.capacity, cp = c / kPipes;
+    WfBufs wbs[kPipes];
+    for (int p = 0; p < kPipes; ++p) {
+      WfBufs& wb = wbs[p];
+      wb.q.a = (float4*)(base + L.q) + p * cp;
+      wb.q.b = (float4*)(base + L.q + sizeof(float4) * c) + p * cp;
+      wb.q.c = (float4*)(base + L.q + 2 * sizeof(float4) * c) + p * cp;
+      wb.hit = (float2*)(base + L.hit) + p * cp;
+      wb.medq = (int32_t*)(base + L.medq) + p * cp;
+      wb.grp = (int2*)(base + L.grp) + p * (cp / 64);
+      wb.staging = (float*)(base + L.staging);
+      wb.next = (int32_t*)(base + L.ctl);
+      wb.ctl = wb.next + (8 + p * kPipeLines) * kLine;
+      wb.capacity = (int32_t)cp;
+      wb.medseg = L.medseg;
+      wb.npix = npix;
+      wb.sq_x = (fr.w + 7) / 8;
+      wb.nsq = wb.sq_x * ((fr.n_rows + 7) / 8);
+      wb.batch = nb;
+      wb.csamp = nb < PTMI_WF_CHUNK_SAMPLES ? nb : PTMI_WF_CHUNK_SAMPLES;
+      wb.nunits = wb.nsq * ((nb + wb.csamp - 1) / wb.csamp) * wb.csamp;
+      wb.shard_len = (wb.nunits / wb.csamp + kShards - 1) / kShards * wb.csamp;
+      wb.shard_groups = L.capacity / 64 / kShards;  // all pipes draw on every shard
+      wb.s_begin = s_begin + b0;
+    }
     hipError_t e;
-    if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wb, accum, nb, counters, stream);
-    else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wb, accum, nb, counters, stream);
-    else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wb, accum, nb, counters, stream);
-    else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wb, accum, nb, counters, stream);
-    else e = wf_batch<64>(sc, fr, wb, accum, nb, counters, stream);
+    if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else e = wf_batch<64>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
