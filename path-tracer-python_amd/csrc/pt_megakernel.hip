@@ -70,6 +70,46 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_BLOCK_WAVES 1  // A/B on MI355X: 1-wave blocks +7 % (C2) / +12 % (C4): a finished wave frees its slot at once
 #endif
 constexpr int kMkBlock = 64 * PTMI_MK_BLOCK_WAVES;
+
+// Staged mode, persistent waves: the grid is one round of the chip's wave
+// slots and every wave draws 64-item units (one 8x8 tile x one sample) from a
+// device counter and refills its lanes across units — no wave ends while work
+// is left, and there is no partly empty last round. Units are tile-major (all
+// samples of a tile are consecutive), and a fetch takes up to
+// PTMI_MK_CHUNK_SAMPLES units while plenty are left, fewer in the tail, so a
+// wave changes tile rarely (lanes of two tiles in one wave fetch more distinct
+// cache lines per load) and the last fetches are small.
+#ifndef PTMI_MK_PERSIST
+#define PTMI_MK_PERSIST 1
+#endif
+#ifndef PTMI_MK_CHUNK_SAMPLES
+#define PTMI_MK_CHUNK_SAMPLES 32  // A/B (C2, C4): 32/4 ~ 16/4 ~ 64/4 > 16/2, 16/8, 8/4 >> 64/2
+#endif
+#ifndef PTMI_MK_TAIL_DIV
+#define PTMI_MK_TAIL_DIV 4  // a fetch takes at most (units left) / (TAIL_DIV * waves) units
+#endif
+// n / d for n < 2^26 by one 64-bit multiply: m = floor(2^(32+l) / d) + 1 with
+// 2^l >= d is exact because n * d < 2^(32+l) (items < 2^32, so units < 2^26).
+struct FastDiv {
+  uint64_t m;
+  uint32_t sh, d;
+};
+static inline FastDiv fast_div(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  return FastDiv{((1ull << (32 + l)) / d) + 1ull, 32u + l, d};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (uint32_t)(((uint64_t)n * f.m) >> f.sh); }
+
+struct MkWork {
+  int32_t* ctl;      // next unit (zeroed before the launch)
+  int32_t csamp;     // most units per fetch
+  int32_t tiles_x;   // 8x8 tiles per row
+  int32_t nb;        // samples of the batch (units per tile)
+  FastDiv by_nb, by_tiles_x;
+  int32_t nunits;    // units of the batch (multiple of csamp)
+  int32_t tail_div;  // TAIL_DIV * waves of the grid
+};
 constexpr int kMkTile = PTMI_MK_BLOCK_WAVES == 4 ? 16 : 8;
 static_assert(PTMI_MK_BLOCK_WAVES == 4 || PTMI_MK_BLOCK_WAVES == 1, "block = 1 or 4 waves");
 
@@ -78,7 +118,8 @@ template <int STACK, bool STAGED>
 // (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the 4-wave VGPR budget of 128
 __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
-    float* __restrict__ staging, unsigned long long* __restrict__ counters) {
+    float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
+  constexpr bool kPersist = STAGED && PTMI_MK_PERSIST;
   __shared__ uint2 lds_stack[STACK * kMkBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
@@ -100,26 +141,47 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   // so all 64 lanes stay busy until the wave's last few paths; any lane may
   // render any item, because colours go to staging[sample][pixel].
   int32_t s0 = s_begin, ns = s_count;
-  if (STAGED) {
+  if (STAGED && !kPersist) {
     s0 = s_begin + (int32_t)blockIdx.z * chunk;
     ns = min(chunk, s_begin + s_count - s0);
   }
   const uint32_t total = 64u * (uint32_t)ns;
   uint32_t next = 64u;  // wave-uniform: next unassigned item
   uint32_t item = (uint32_t)lane;
+  uint32_t wend = 0u;   // persistent: end of the wave's current units (items)
+  bool drained = false; // persistent: the batch's units are all handed out
   int32_t px = 0, py = -1, lr = 0, s = s0;
   float* ap = nullptr;
   pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
   bool live = false;
-  auto bind = [&](uint32_t k) -> bool {  // item -> pixel/sample; false if the pixel is outside the frame
+  // item -> tile origin (x, local row) and sample; persistent items are
+  // unit-major: unit u = chunk u / csamp (tile chunk % ntiles, sample block
+  // chunk / ntiles), sample u % csamp of the block
+  struct Loc {
+    int32_t x, row, s;  // tile origin (image x, local row), sample
+  };
+  auto locate = [&](uint32_t k) -> Loc {
+    if (kPersist) {
+      const uint32_t u = k >> 6, t = fdiv(u, wk.by_nb), ty = fdiv(t, wk.by_tiles_x);
+      return Loc{fr.x0 + (int32_t)(t - ty * (uint32_t)wk.tiles_x) * 8, (int32_t)ty * 8,
+                 s_begin + (int32_t)(u - t * (uint32_t)wk.nb)};
+    }
+    return Loc{sq_x, sq_y, s0 + (int32_t)(k >> 6)};
+  };
+  auto bind = [&](uint32_t k) -> bool {  // item -> pixel/sample; false if outside the frame / batch
     const int32_t p = (int32_t)(k & 63u);
-    px = sq_x + (p & 7);
-    lr = sq_y + (p >> 3);
-    s = s0 + (int32_t)(k >> 6);
-    py = (lr < fr.n_rows && px < fr.x0 + fr.w) ? frame_row(fr, lr) : -1;
+    const Loc l = locate(k);
+    s = l.s;
+    px = l.x + (p & 7);
+    lr = l.row + (p >> 3);
+    py = (lr < fr.n_rows && px < fr.x0 + fr.w && s < s_begin + s_count) ? frame_row(fr, lr) : -1;
     return py >= 0;
   };
-  if (item < total && bind(item)) {
+  if (kPersist) {  // first units of the wave
+    next = 0u;
+    item = 0xffffffffu;
+  }
+  if (!kPersist && item < total && bind(item)) {
     if (!STAGED) {
       ap = accum + 3 * ((size_t)py * (size_t)fr.width + (size_t)px);
       acc = pt_v3f(ap[0], ap[1], ap[2]);
@@ -242,9 +304,10 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
         if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
           // slot of this lane's item (recomputed: pixel/sample need not stay live)
           const int32_t ip = (int32_t)(item & 63u);
-          const size_t srel = (size_t)(s0 - s_begin) + (size_t)(item >> 6);
-          float* o = staging + 3 * (srel * npix + (size_t)(sq_y + (ip >> 3)) * (size_t)fr.w +
-                                    (size_t)(sq_x + (ip & 7) - fr.x0));
+          const Loc l = locate(item);
+          const size_t srel = (size_t)(l.s - s_begin);
+          float* o = staging + 3 * (srel * npix + (size_t)(l.row + (ip >> 3)) * (size_t)fr.w +
+                                    (size_t)(l.x + (ip & 7) - fr.x0));
           o[0] = ps.color.x;
           o[1] = ps.color.y;
           o[2] = ps.color.z;
@@ -262,7 +325,48 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
         begin_segment();  // next segment of this path (or its medium exit search)
       }
     }
-    if (STAGED) {  // hand the wave's next items to the lanes without a path
+    if (kPersist) {  // hand the wave's next items to the lanes without a path, fetching units as needed
+      const unsigned long long want = __ballot(!live);
+      if (want && !(drained && next >= wend)) {
+        const uint32_t n = (uint32_t)__popcll(want);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+        const uint32_t avail = wend - next;
+        uint32_t my = rank < avail ? next + rank : 0xffffffffu;
+        if (n > avail && !drained) {  // one fetch covers it: a unit is 64 items
+          int32_t u0 = 0;
+          if (lane == 0) {
+            const int32_t cur = __hip_atomic_load(wk.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int32_t take = max(1, min(wk.csamp, (wk.nunits - cur) / wk.tail_div));
+            u0 = cur < wk.nunits ? atomicAdd(wk.ctl, take) : wk.nunits;
+            const int32_t u1 = min(u0 + take, wk.nunits);
+            u0 = u0 < wk.nunits ? u0 : -1;
+            if (u0 >= 0) wend = 64u * (uint32_t)u1;  // lane 0's copy, broadcast below
+          }
+          u0 = __shfl(u0, 0);
+          wend = __shfl(wend, 0);
+          if (u0 >= 0) {
+            const uint32_t cb = 64u * (uint32_t)u0;
+            if (rank >= avail) my = cb + (rank - avail);
+            next = cb + (n - avail);
+          } else {
+            drained = true;
+            next = wend;
+          }
+        } else {
+          next = n > avail ? wend : next + n;
+        }
+        if (!live && my != 0xffffffffu) {
+          item = my;
+          if (bind(item)) {
+            start_path(fr, px, py, s, ps);
+            live = true;
+            begin_segment();
+          }
+        }
+      }
+      if (__ballot(live) == 0ull && drained && next >= wend) break;
+    } else if (STAGED) {  // hand the wave's next items to the lanes without a path
       const unsigned long long want = __ballot(!live);
       if (want && next < total) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
@@ -339,7 +443,7 @@ static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum
   dim3 grid((unsigned)((fr.w + kMkTile - 1) / kMkTile), (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile));
   prof_begin(kProfMk, stream);
   hipLaunchKernelGGL((mk_render_kernel<STACK, false>), grid, dim3(kMkBlock), 0, stream, sc, fr, accum, s_begin,
-                     s_count, s_count, (float*)nullptr, counters);
+                     s_count, s_count, (float*)nullptr, counters, MkWork{});
   prof_end(kProfMk, stream);
   return hipGetLastError();
 }
@@ -365,9 +469,13 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
 #define PTMI_MK_DIRECT_MIN_TILES 0x7fffffff  // A/B: staged + item pool beat direct even at 4K (+3 %)
 #endif
 
-size_t mk_workspace_bytes(int32_t npix, int32_t batch) {
-  if (npix <= 0 || batch <= 0) return 0;
+static size_t mk_staging_bytes(int32_t npix, int32_t batch) {
   return (3 * sizeof(float) * (size_t)npix * (size_t)batch + 255) & ~(size_t)255;
+}
+
+size_t mk_workspace_bytes(int32_t npix, int32_t batch) {  // staging + one 256-B counter line
+  if (npix <= 0 || batch <= 0) return 0;
+  return mk_staging_bytes(npix, batch) + 256;
 }
 
 template <int STACK>
@@ -375,6 +483,36 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
                                    int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream) {
   const unsigned tx = (unsigned)((fr.w + kMkTile - 1) / kMkTile), ty = (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile);
   const int64_t tiles = (int64_t)tx * ty;
+#if PTMI_MK_PERSIST
+  static_assert(PTMI_MK_BLOCK_WAVES == 1, "persistent staged mode uses one-wave blocks");
+  int dev = 0, ncu = 0, per_cu = 0;
+  hipError_t e0 = hipGetDevice(&dev);
+  if (e0 == hipSuccess) e0 = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e0 == hipSuccess)
+    e0 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk_render_kernel<STACK, true>, kMkBlock, 0);
+  if (e0 != hipSuccess) return e0;
+  MkWork wk;
+  wk.ctl = (int32_t*)((char*)staging + mk_staging_bytes(fr.w * fr.n_rows, nb));
+  wk.csamp = PTMI_MK_CHUNK_SAMPLES;
+  wk.tiles_x = (int32_t)tx;
+  wk.nb = nb;
+  if (tiles * nb * 64 >= (1ll << 32)) return hipErrorInvalidValue;  // item ids are 32-bit
+  wk.nunits = (int32_t)(tiles * nb);
+  wk.by_nb = fast_div((uint32_t)nb);
+  wk.by_tiles_x = fast_div((uint32_t)wk.tiles_x);
+#ifdef PTMI_MK_PERSIST_WPC
+  per_cu = PTMI_MK_PERSIST_WPC;
+#endif
+  int64_t waves = (int64_t)(per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
+  const int64_t chunks = wk.nunits;
+  if (waves > chunks) waves = chunks;
+  wk.tail_div = (int32_t)(PTMI_MK_TAIL_DIV * waves);
+  (void)hipMemsetAsync(wk.ctl, 0, sizeof(int32_t), stream);
+  prof_begin(kProfMk, stream);
+  hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
+                     sc, fr, accum, s_begin, nb, nb, staging, counters, wk);
+  prof_end(kProfMk, stream);
+#else
   int64_t nchunks = (PTMI_MK_TARGET_BLOCKS + tiles - 1) / tiles;
   if (nchunks < 1) nchunks = 1;
   if (nchunks > nb) nchunks = nb;
@@ -382,8 +520,9 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   nchunks = (nb + chunk - 1) / chunk;
   prof_begin(kProfMk, stream);
   hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3(tx, ty, (unsigned)nchunks), dim3(kMkBlock), 0, stream,
-                     sc, fr, accum, s_begin, nb, chunk, staging, counters);
+                     sc, fr, accum, s_begin, nb, chunk, staging, counters, MkWork{});
   prof_end(kProfMk, stream);
+#endif
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_stage_resolve(fr, staging, fr.w * fr.n_rows, nb, accum, kProfMkResolve, stream);
