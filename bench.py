@@ -211,7 +211,14 @@ def main():
     if world > 1:
         dist.barrier()
 
-    with _lib.KernelTimer(max_launches=100_000) as kt:
+    # Per-kernel durations (roofline): HIP events around every launch, on the
+    # stream it runs on. The megakernel (2 events per 18-ms launch) is timed
+    # inside the timed region. The wavefront's pipes are concurrent streams and
+    # an event per launch costs them ~10 %, so its kernels are timed in a
+    # second pass over the same K steps into a scratch accumulator and the
+    # timed region runs without events.
+    inline = a.variant == 'mk'
+    with _lib.KernelTimer(max_launches=100_000 if inline else 0) as kt:
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -225,6 +232,13 @@ def main():
         elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dev if a.dist_backend == 'nccl' else None)
     cnt = integ.read_counters()
+    if not inline:
+        acc_k = torch.zeros_like(acc)
+        with _lib.KernelTimer(max_launches=100_000) as kt:
+            for k in range(a.steps):
+                render(frame, acc_k, sample_base(a.warmup + k), sps)
+            torch.cuda.synchronize(dev)
+        del acc_k
     rows_rank = len(shard.rows(H))
     samples_rank = W * rows_rank * sps * a.steps
     samples_all = samples_rank * world if a.shard == 'samples' else W * H * sps * a.steps
@@ -279,6 +293,8 @@ def main():
             'avg_launch_ms': round(dom_ms / max(1, launches), 5),
             'launches': launches,
             'timing_truncated': bool(kt.truncated),
+            'timing': ('HIP events per launch on its stream, in the timed region' if inline else
+                       'HIP events per launch on its stream, in a second pass over the same steps'),
         },
         'kernels_ms': {k: round(v['ms'], 3) for k, v in prof.items() if v['launches']},
         'segments_per_sample': round(S, 4),

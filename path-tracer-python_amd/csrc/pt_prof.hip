@@ -56,9 +56,10 @@ int prof_stop(double* ms, uint64_t* launches, int32_t n_kinds) {
     launches[k] = 0;
   }
   int rc = g_prof.overflow ? 1 : 0;
-  if (g_prof.used >= 2 && hipEventSynchronize(g_prof.ev[g_prof.used - 1]) != hipSuccess) rc = -1;
   for (size_t p = 0; p + 1 < g_prof.used; p += 2) {
     float t = 0.0f;
+    // launches may sit on several streams (wavefront pipes): wait for each
+    if (hipEventSynchronize(g_prof.ev[p + 1]) != hipSuccess) { rc = -1; continue; }
     if (hipEventElapsedTime(&t, g_prof.ev[p], g_prof.ev[p + 1]) != hipSuccess) { rc = -1; continue; }
     int32_t k = g_prof.kind[p / 2];
     if (k >= 0 && k < n_kinds) {

@@ -28,6 +28,10 @@ for s in "$@"; do
     rocprofwf) step rocprofwf 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o benchwf -- python bench.py --variant wf --no-cpu-baseline ;;
     traffic) step trafficf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic -o fetch -- python bench.py --steps 4 --no-cpu-baseline && step trafficw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/traffic -o write -- python bench.py --steps 4 --no-cpu-baseline ;;
     trafficwf) step trafficwff 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic -o wffetch -- python bench.py --variant wf --steps 4 --no-cpu-baseline && step trafficwfw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/traffic -o wfwrite -- python bench.py --variant wf --steps 4 --no-cpu-baseline ;;
+    trafficp) for pr in ${TRAFFIC_PRESETS:-c4 c5}; do
+               step traffic${pr}f 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic -o ${pr}fetch -- python bench.py --preset $pr --steps 4 --no-cpu-baseline || exit 1
+               step traffic${pr}w 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/traffic -o ${pr}write -- python bench.py --preset $pr --steps 4 --no-cpu-baseline || exit 1
+             done ;;
     ab) step ab 900 bash tools/gpu_ab.sh ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc) step pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc -o pass1 -- python tools/ab.py mk 32 1 && step pmc2 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o pass2 -- python tools/ab.py mk 32 1 && step pmc3 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o pass3 -- python tools/ab.py mk 32 1 ;;
