@@ -7,7 +7,9 @@
  * reference, so each entry point below names the reference launch/host site it
  * replaces. Plain C types only: device pointers are raw pointers owned by the
  * caller (the Python host allocates them as torch tensors); the library never
- * allocates inside a render call. All functions return 0 on success and a
+ * allocates device memory inside a render call (it owns one pinned readback
+ * slot and, per device, the wavefront's 3 extra streams, created on first
+ * use). All functions return 0 on success and a
  * negative PTMI_E* code on error; ptmi_last_error() gives a message.
  */
 #ifndef PTMI_H
@@ -116,14 +118,15 @@ int ptmi_scene_check(const ptmi_scene_view *scene);
 int ptmi_mk_render(const ptmi_scene_view *scene, const ptmi_frame *frame, float *accum,
                    int32_t sample_begin, int32_t sample_count, uint64_t *counters, void *stream);
 
-/* Megakernel over (16x16 tile, chunk of samples) work units — enough units
- * to fill the chip for ~16 rounds, so a launch does not end in a long,
- * partially occupied last round. Each path's colour goes to a staging slot
- * [sample][pixel] of `workspace` and a resolve kernel adds them into accum in
- * sample order: same results, bit for bit, as ptmi_mk_render. workspace:
- * device memory (16-byte aligned) of at least ptmi_mk_workspace_bytes(frame, 1)
- * bytes; ptmi_mk_workspace_bytes(frame, B) = 12 * pixels * B (rounded up)
- * lets one batch hold B samples. Asynchronous, graph-capturable. */
+/* Megakernel with persistent waves: one round of the chip's wave slots, each
+ * wave drawing (8x8 tile, sample) units from a device counter in `workspace`
+ * until the batch is done, so a launch has no partly occupied last round.
+ * Each path's colour goes to a staging slot [sample][pixel] of `workspace`
+ * and a resolve kernel adds them into accum in sample order: same results,
+ * bit for bit, as ptmi_mk_render. workspace: device memory (16-byte aligned)
+ * of at least ptmi_mk_workspace_bytes(frame, 1) bytes;
+ * ptmi_mk_workspace_bytes(frame, B) = 12 * pixels * B (rounded up to 256) +
+ * 256 lets one batch hold B samples. Asynchronous, graph-capturable. */
 size_t ptmi_mk_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_mk_render_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                       size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
@@ -137,8 +140,12 @@ int ptmi_mk_render_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, voi
  * (16-byte aligned) of at least ptmi_wf_workspace_bytes(frame, 1) bytes;
  * ptmi_wf_workspace_bytes(frame, B) bytes let one batch hold B samples of
  * every pixel (ray queues + a per-(sample, pixel) staging slot). Larger
- * sample counts run in batches. Synchronises the stream once every few
- * queue iterations to read the live-ray count (not graph-capturable). */
+ * sample counts run in batches. The queue runs as 4 independent pipes: pipe 0
+ * on `stream`, pipes 1-3 on library-owned streams forked from `stream` and
+ * joined back into it with events, so the work is ordered after earlier and
+ * before later work on `stream` like one launch. Synchronises the pipes once
+ * every few queue iterations to read their live-ray counts (not
+ * graph-capturable). */
 size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
