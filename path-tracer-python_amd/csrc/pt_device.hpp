@@ -129,6 +129,9 @@ __device__ __forceinline__ void get_ray(const DevFrame& fr, int32_t px, int32_t 
 }
 
 // ---------------------------------------------------------------- primitives
+#ifndef PTMI_LEAF_PRELOAD
+#define PTMI_LEAF_PRELOAD 1  // A/B on MI355X: +1.4 % C2, +4 % C4, +2.6 % wavefront
+#endif
 // Each returns the candidate t (hit only if returned true); hit point and
 // normal are recomputed at shading time from (o, d, t) with the same
 // operation order the reference uses inside the hit functions.
@@ -152,7 +155,17 @@ __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, f
 
 __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o, pt_v3 d, float tmin,
                                            float tmax, float& t) {  // kernels.py:311-362
+#if PTMI_LEAF_PRELOAD
+  // all 64 B in one round trip (the compiler otherwise sinks the loads into
+  // the branches: three dependent L2 round trips per quad test)
+  typedef float pt_f4 __attribute__((ext_vector_type(4)));
+  pt_f4 A = ((const pt_f4*)q)[0], B = ((const pt_f4*)q)[1], C = ((const pt_f4*)q)[2], E = ((const pt_f4*)q)[3];
+  asm volatile("" : "+v"(A), "+v"(B), "+v"(C), "+v"(E));
+  const float4 a = make_float4(A.x, A.y, A.z, A.w), b = make_float4(B.x, B.y, B.z, B.w);
+  const float4 c = make_float4(C.x, C.y, C.z, C.w), e = make_float4(E.x, E.y, E.z, E.w);
+#else
   float4 a = q[0], b = q[1], c = q[2], e = q[3];
+#endif
   pt_v3 n = pt_v3f(a.x, a.y, a.z);
   float denom = pt_dot(n, d);
   if (fabsf(denom) >= 1e-8f) {
@@ -172,7 +185,15 @@ __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o
 
 __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
                                           float tmax, float& t) {  // kernels.py:252-307
+#if PTMI_LEAF_PRELOAD
+  typedef float pt_f4 __attribute__((ext_vector_type(4)));
+  pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1], C = ((const pt_f4*)tr)[2];
+  asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
+  const float4 a = make_float4(A.x, A.y, A.z, A.w), b = make_float4(B.x, B.y, B.z, B.w);
+  const float4 c = make_float4(C.x, C.y, C.z, C.w);
+#else
   float4 a = tr[0], b = tr[1], c = tr[2];
+#endif
   pt_v3 v0 = pt_v3f(a.x, a.y, a.z), e1 = pt_v3f(a.w, b.x, b.y), e2 = pt_v3f(b.z, b.w, c.x);
   pt_v3 hv = pt_cross(d, e2);
   float det = pt_dot(e1, hv);
@@ -271,8 +292,11 @@ __device__ unsigned long long g_probe[8];
 #define PTMI_NODE_CENTRES 1
 #endif
 
+#ifndef PTMI_NODES_SGPR
+#define PTMI_NODES_SGPR 1  // megakernel: node base pinned in SGPRs (A/B with leaf preload: +0.8 % C2/C4)
+#endif
 #ifndef PTMI_NODES_VGPR
-#define PTMI_NODES_VGPR 1  // A/B on MI355X: +2 % megakernel
+#define PTMI_NODES_VGPR (!PTMI_NODES_SGPR)  // A/B on MI355X: +2 % megakernel
 #endif
 
 // In-flight traversal of one ray: begin (root test, push root) and one pop
@@ -320,12 +344,13 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // half of the visited entries are leaves, and a wave's lanes no longer split
 // between "leaf" and "node" iterations.
 template <int STACK, int SB = kBlock>
-__device__ __forceinline__ void trav_step(const DevScene& sc, Trav& tr, Stack st, pt_v3 o, pt_v3 d) {
+__device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
+                                          pt_v3 d) {
   // global address space: global_load, not flat_load (a laundered generic
   // pointer would otherwise lose it); clang vector type, no C++ copy ctor
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) pt_f4 gf4;
-  gf4* nodes = (gf4*)sc.nodes;
+  gf4* nodes = (gf4*)node_base;
 #if PTMI_NODES_VGPR
   // keep the node base in VGPRs: under SGPR pressure the compiler otherwise
   // re-loads it from the kernarg segment on every visit (s_load + lgkmcnt wait
@@ -424,7 +449,7 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, f
                                          float& t_out, int32_t& ref_out) {
   Trav tr;
   trav_begin<STACK, SB>(sc, tr, st, d, o, tmin, tmax);
-  while (tr.busy()) trav_step<STACK, SB>(sc, tr, st, o, d);
+  while (tr.busy()) trav_step<STACK, SB>(sc, sc.nodes, tr, st, o, d);
   t_out = tr.closest;
   ref_out = tr.best;
   return tr.any();

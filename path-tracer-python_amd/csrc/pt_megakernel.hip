@@ -120,6 +120,17 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
   constexpr bool kPersist = STAGED && PTMI_MK_PERSIST;
+  const float4* nodes = sc.nodes;
+#if PTMI_NODES_SGPR
+  {  // node base pinned in an SGPR pair for the whole kernel: under SGPR
+     // pressure the compiler otherwise re-loads it from the kernarg segment on
+     // every traversal step (s_load + lgkmcnt wait on the pop's critical path)
+    const uint64_t nb = (uint64_t)nodes;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)nb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(nb >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    nodes = (const float4*)(((uint64_t)hi << 32) | lo);
+  }
+#endif
   __shared__ uint2 lds_stack[STACK * kMkBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
@@ -215,7 +226,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
       const int nbusy = __popcll(__ballot(trav && tr.busy()));
       if (nbusy == 0) break;
       if (nbusy <= PTMI_MK_SHADE_AT && __ballot(trav && !tr.busy()) != 0ull) break;
-      if (trav && tr.busy()) trav_step<STACK, kMkBlock>(sc, tr, st, ps.o, ps.dir);
+      if (trav && tr.busy()) trav_step<STACK, kMkBlock>(sc, nodes, tr, st, ps.o, ps.dir);
     }
     if (trav && !tr.busy()) {  // segment traced: shade it
       trav = false;
