@@ -262,7 +262,9 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // while-while -15 %; persistent lanes refilled per ray (wf) -7 %; skipping
 // culled pops in an inner loop -11 %; scalar-cache fetch of wave-uniform
 // nodes -1.7 % (the SGPR->VGPR moves cost more VALU than the texture path
-// saves). Kept: packed pairs, precomputed centres, branch-free pushes.
+// saves); testing a leaf pushed on top in the expanding step itself -3 % mk
+// (profiles/r01/ab_leaf_top.log). Kept: packed pairs, precomputed centres,
+// branch-free pushes.
 
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
 
