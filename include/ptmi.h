@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 3
+#define PTMI_ABI_VERSION 4
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -43,7 +43,9 @@ enum {
  *             min.z c0,c1, max.x c0,c1 | max.y c0,c1, max.z c0,c1 |
  *             ref0, ref1 (i32 bits), centre.z c0,c1 | centre.x c0,c1,
  *             centre.y c0,c1}; centre = (min + max) * 0.5f in f32.
- *             ref >= 0: internal node index; ref < 0: leaf code
+ *             ref >= 0: internal node, as its BYTE offset in nodes
+ *             (index x 80: the traversal adds it to the node base with
+ *             no index scaling); ref < 0: leaf code
  *             0x80000000 | type << 28 | prim index (type: 0 sphere,
  *             1 triangle, 2 quad — scene_compiler.py:10-12).
  *   spheres : ns x 4 f32 {cx, cy, cz, r}                (fields.py:25)

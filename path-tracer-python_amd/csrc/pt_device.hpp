@@ -272,6 +272,23 @@ struct Stack {
   uint2* slot0;  // &lds[tid]; slot k at slot0[k * SB] (SB = threads per block)
 };
 
+// LDS accesses by 32-bit byte address (a stack pointer kept as the address of
+// its slot: one v_add per pop or push, no index scaling).
+typedef uint32_t pt_u2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) pt_u2v pt_lds_u2v;
+typedef __attribute__((address_space(3))) uint32_t pt_lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(uint2* p) { return (uint32_t)(uintptr_t)(pt_lds_u2v*)p; }
+__device__ __forceinline__ pt_u2v lds_load2(uint32_t a) { return *(pt_lds_u2v*)(uintptr_t)a; }
+__device__ __forceinline__ void lds_store2(uint32_t a, uint32_t x, uint32_t y) {
+  pt_lds_u32* q = (pt_lds_u32*)(uintptr_t)a;
+  q[0] = x;
+  q[1] = y;
+}
+
+// Lane mask of a predicate (v_cmp straight into an SGPR pair; __ballot's int
+// argument costs a v_cndmask + v_cmp per call).
+__device__ __forceinline__ unsigned long long pt_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ void slab(pt_v3 o, pt_v3 inv, float mnx, float mny, float mnz, float mxx, float mxy,
                                      float mxz, float tmin, float& E, float& X) {
   float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
@@ -308,15 +325,12 @@ struct Trav {
   pt_v3 inv;
   float tmin, closest;
   int32_t best;  // leaf code of the closest hit; 0 = none (leaf codes are negative)
-  int32_t sp;
-  int32_t pend;  // popped leaf whose test runs at the start of the next step; 0 = none
+  uint32_t sp;   // LDS byte address of the next free stack slot
+  uint32_t sp0;  // LDS byte address of slot 0: the stack is empty when sp == sp0
   __device__ __forceinline__ bool any() const { return best != 0; }
-  __device__ __forceinline__ bool busy() const { return sp > 0 || pend != 0; }
+  __device__ __forceinline__ bool busy() const { return sp != sp0; }
+  __device__ __forceinline__ void init(Stack st) { sp = sp0 = lds_addr(st.slot0); }
 };
-
-#ifndef PTMI_LEAF_DEFER
-#define PTMI_LEAF_DEFER 0  // A/B on MI355X: deferring leaf tests to the next step -5 % mk, -3.5 % wf
-#endif
 
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack st, pt_v3 d, pt_v3 o, float tmin,
@@ -326,25 +340,21 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
   tr.tmin = tmin;
   tr.closest = tmax;
   tr.best = 0;
-  tr.sp = 0;
-  tr.pend = 0;
+  tr.init(st);
   if (sc.n_inner == 0 && sc.root_ref >= 0) return;  // empty scene
   float E, X;
   slab(o, tr.inv, sc.root_min[0], sc.root_min[1], sc.root_min[2], sc.root_max[0], sc.root_max[1], sc.root_max[2],
        tmin, E, X);
   if (pt_minf(X, tr.closest) >= E) {
-    st.slot0[0] = make_uint2((uint32_t)sc.root_ref, __float_as_uint(E));
-    tr.sp = 1;
+    lds_store2(tr.sp, (uint32_t)sc.root_ref, __float_as_uint(E));
+    tr.sp += SB * 8;
   }
 }
 
-// One step of the traversal loop; precondition tr.busy(). With
-// PTMI_LEAF_DEFER a popped leaf is tested at the start of the NEXT step, before
-// that step's pop and its cull test — the same order of leaf tests, culls and
-// closest-hit updates as testing it at once — so one step can run a leaf test
-// and a node expansion for the same lane: with one primitive per leaf, about
-// half of the visited entries are leaves, and a wave's lanes no longer split
-// between "leaf" and "node" iterations.
+// One step of the traversal loop (one pop); precondition tr.busy().
+// A/B on MI355X (parity-identical): deferring a popped leaf's test to the next
+// step -5 % mk / -3.5 % wf; testing a just-pushed leaf in the expanding step
+// -3 % mk (profiles/r01/ab_leaf_top.log).
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
@@ -359,19 +369,9 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   // on the pop's critical path)
   asm volatile("" : "+v"(nodes));
 #endif
-#if PTMI_LEAF_DEFER
-  if (tr.pend != 0) {  // leaf: kernels.py:671-697
-    float t;
-    if (hit_leaf(sc, tr.pend, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
-      tr.closest = t;
-      tr.best = tr.pend;
-    }
-    tr.pend = 0;
-  }
-  if (tr.sp == 0) return;
-#endif
-  --tr.sp;
-  const uint2 ent = st.slot0[tr.sp * SB];
+  constexpr uint32_t kSlot = SB * 8;  // bytes between a lane's consecutive slots
+  tr.sp -= kSlot;
+  const pt_u2v ent = lds_load2(tr.sp);
   const int32_t ref = (int32_t)ent.x;
 #if PTMI_PROBE
   atomicAdd(&g_probe[4], 1ull);                                                    // pops
@@ -380,15 +380,11 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
 #endif
   if (!(__uint_as_float(ent.y) <= tr.closest)) return;
   if (ref < 0) {
-#if PTMI_LEAF_DEFER
-    tr.pend = ref;
-#else
     float t;  // leaf: kernels.py:671-697
     if (hit_leaf(sc, ref, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
       tr.closest = t;
       tr.best = ref;
     }
-#endif
     return;
   }
 #if PTMI_PROBE
@@ -409,7 +405,7 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
   const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
   const float tmin = tr.tmin;
-  gf4* nd = nodes + 5 * ref;  // 80-B node
+  gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // 80-B node at byte offset ref
   const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
   const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
   const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
@@ -429,21 +425,24 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
 #endif
   const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
-  const bool ln = dist.x < dist.y;
-  const int32_t r0 = __float_as_int(R.x), r1 = __float_as_int(R.y);
-  const int32_t fr = ln ? r1 : r0, nr = ln ? r0 : r1;
-  const float fE = ln ? E1 : E0, nE = ln ? E0 : E1;
+  const bool ln = dist.x < dist.y;  // child 0 is the near one; the far child is pushed first
   const bool h0 = X0 >= E0, h1 = X1 >= E1;
-  const bool fh = ln ? h1 : h0, nh = ln ? h0 : h1;
-  // Far first, then near; each slot written unconditionally and kept only if
-  // its child is hit. No bound check: an internal node at depth d has at most
-  // d pending entries, so sp + 2 <= max_leaf_depth + 1 <= STACK always
-  // (STACK >= max_leaf_depth + 1 is enforced at dispatch) and the
-  // reference's overflow drop can never trigger.
-  st.slot0[tr.sp * SB] = make_uint2((uint32_t)fr, __float_as_uint(fE));
-  tr.sp += fh ? 1 : 0;
-  st.slot0[tr.sp * SB] = make_uint2((uint32_t)nr, __float_as_uint(nE));
-  tr.sp += nh ? 1 : 0;
+  // Far first, then near, each kept only if its box is hit: the far child
+  // lands at sp and the near one at sp + slot when the far one is hit, else
+  // the near one at sp and the (dropped) far one at sp + slot, above the
+  // top. Child 0 takes the upper slot when (near and the far child 1 is hit)
+  // or (far and missed). Writing each child's {ref, E} straight to its slot
+  // needs no value selects. No bound check: an internal node at depth d has
+  // at most d pending entries, so sp + 2 slots <= max_leaf_depth + 1 <= STACK
+  // (enforced at dispatch) and the reference's overflow drop never triggers.
+  // up0 = ln ? h1 : !h0, as and/or of the compares' lane masks (SALU; a bool
+  // select would be materialised with four v_cndmask)
+  const unsigned long long mln = pt_ballot(ln), mh0 = pt_ballot(h0), mh1 = pt_ballot(h1);
+  const bool up0 = __builtin_amdgcn_inverse_ballot_w64((mln & mh1) | (~mln & ~mh0));
+  const uint32_t lo = tr.sp, hi = tr.sp + kSlot;
+  lds_store2(up0 ? hi : lo, __float_as_uint(R.x), __float_as_uint(E0));
+  lds_store2(up0 ? lo : hi, __float_as_uint(R.y), __float_as_uint(E1));
+  tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
 }
 
 template <int STACK, int SB = kBlock>

@@ -210,8 +210,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   // of the whole wave idling until its longest traversal ends (node steps ran
   // at ~35 % SIMD efficiency that way). 0 = wait for every lane.
   Trav tr;
-  tr.sp = 0;
-  tr.pend = 0;
+  tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
@@ -223,10 +222,13 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
 
   for (;;) {
     for (;;) {  // traversal steps
-      const int nbusy = __popcll(__ballot(trav && tr.busy()));
+      // a lane's stack is empty unless its segment is mid-traversal (busy => trav)
+      const unsigned long long mbusy = pt_ballot(tr.busy());
+      // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
+      const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      if (nbusy <= PTMI_MK_SHADE_AT && __ballot(trav && !tr.busy()) != 0ull) break;
-      if (trav && tr.busy()) trav_step<STACK, kMkBlock>(sc, nodes, tr, st, ps.o, ps.dir);
+      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
+      if (tr.busy()) trav_step<STACK, kMkBlock>(sc, nodes, tr, st, ps.o, ps.dir);
     }
     if (trav && !tr.busy()) {  // segment traced: shade it
       trav = false;

@@ -174,6 +174,7 @@ LEAF_FLAG = np.int64(0x80000000)
 
 
 NODE_FLOATS = 20  # 80-B internal node (include/ptmi.h)
+NODE_BYTES = 4 * NODE_FLOATS  # an internal child ref is the child's byte offset in the node array
 
 
 def leaf_code(prim_type, prim_idx):
@@ -265,7 +266,9 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
     cidx = np.full(n, -1, np.int64)
     cidx[internal] = np.arange(internal.shape[0])
     codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | pidx.astype(np.int64)) - (1 << 32)).astype(np.int32)
-    refs = np.where(is_leaf, codes, cidx.astype(np.int32)).astype(np.int32)
+    if internal.shape[0] * NODE_BYTES > 0x7fffffff:
+        raise ValueError(f'{internal.shape[0]} internal BVH nodes: byte offsets exceed int32')
+    refs = np.where(is_leaf, codes, (cidx * NODE_BYTES).astype(np.int32)).astype(np.int32)
     nodes = np.zeros((internal.shape[0], NODE_FLOATS), np.float32)
     if internal.size:  # children interleaved per component (include/ptmi.h)
         l, r = left[internal], right[internal]
