@@ -354,7 +354,10 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // One step of the traversal loop (one pop); precondition tr.busy().
 // A/B on MI355X (parity-identical): deferring a popped leaf's test to the next
 // step -5 % mk / -3.5 % wf; testing a just-pushed leaf in the expanding step
-// -3 % mk (profiles/r01/ab_leaf_top.log).
+// -3 % mk (profiles/r01/ab_leaf_top.log). Sphere roots through a per-ray
+// reciprocal of dot(d, d) (Markstein's fma sequence, bit-exact) and sqrt
+// without the tiny/inf fix-ups: 14-20 VALU fewer per sphere test, and no
+// faster (-0.5 %; profiles/r01/ab_fast_div_sqrt.log).
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
