@@ -304,7 +304,7 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 #define PTMI_PROBE 0
 #endif
 #if PTMI_PROBE
-__device__ unsigned long long g_probe[8];
+__device__ unsigned long long g_probe[16];
 #endif
 
 #ifndef PTMI_NODE_CENTRES
@@ -327,6 +327,9 @@ struct Trav {
   int32_t best;  // leaf code of the closest hit; 0 = none (leaf codes are negative)
   uint32_t sp;   // LDS byte address of the next free stack slot
   uint32_t sp0;  // LDS byte address of slot 0: the stack is empty when sp == sp0
+#if PTMI_PROBE == 2
+  uint32_t probe;  // branches this lane took in the current step: 1 sphere, 2 quad/tri, 4 node
+#endif
   __device__ __forceinline__ bool any() const { return best != 0; }
   __device__ __forceinline__ bool busy() const { return sp != sp0; }
   __device__ __forceinline__ void init(Stack st) { sp = sp0 = lds_addr(st.slot0); }
@@ -357,7 +360,10 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // -3 % mk (profiles/r01/ab_leaf_top.log). Sphere roots through a per-ray
 // reciprocal of dot(d, d) (Markstein's fma sequence, bit-exact) and sqrt
 // without the tiny/inf fix-ups: 14-20 VALU fewer per sphere test, and no
-// faster (-0.5 %; profiles/r01/ab_fast_div_sqrt.log).
+// faster (-0.5 %; profiles/r01/ab_fast_div_sqrt.log). One 80-B fetch per
+// popped entry, node or primitive, issued before the node/leaf branch (one
+// L2 wait per mixed step instead of two): -4.6 % mk, -14 % wf
+// (profiles/r01/ab_unified_fetch.log).
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
@@ -377,12 +383,17 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const pt_u2v ent = lds_load2(tr.sp);
   const int32_t ref = (int32_t)ent.x;
 #if PTMI_PROBE
+#if PTMI_PROBE == 1
   atomicAdd(&g_probe[4], 1ull);                                                    // pops
   if (!(__uint_as_float(ent.y) <= tr.closest)) atomicAdd(&g_probe[5], 1ull);       // culled pops
   else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
 #endif
+#endif
   if (!(__uint_as_float(ent.y) <= tr.closest)) return;
   if (ref < 0) {
+#if PTMI_PROBE == 2
+    tr.probe |= leaf_type(ref) == kSphere ? 1 : 2;
+#endif
     float t;  // leaf: kernels.py:671-697
     if (hit_leaf(sc, ref, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
       tr.closest = t;
@@ -390,7 +401,10 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     }
     return;
   }
-#if PTMI_PROBE
+#if PTMI_PROBE == 2
+  tr.probe |= 4;
+#endif
+#if PTMI_PROBE == 1
   {  // debug probe: node visits and wave-uniform node visits (lane counts)
     const int32_t ru = __builtin_amdgcn_readfirstlane(ref);
     const bool uni = __ballot(ref != ru) == 0ull;

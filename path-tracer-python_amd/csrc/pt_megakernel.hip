@@ -220,6 +220,12 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   };
   if (live) begin_segment();
 
+#if PTMI_PROBE == 2
+  // wave-level probe (diagnostic build): shader cycles in the traversal-step
+  // loop and in shading/refill; wave steps and the branches they ran
+  uint64_t pr_trav = 0, pr_shade = 0, pr_steps = 0, pr_sph = 0, pr_oth = 0, pr_node = 0;
+  uint64_t pr_t = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     for (;;) {  // traversal steps
       // a lane's stack is empty unless its segment is mid-traversal (busy => trav)
@@ -228,8 +234,24 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
       if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
+#if PTMI_PROBE == 2
+      tr.probe = 0;
+#endif
       if (tr.busy()) trav_step<STACK, kMkBlock>(sc, nodes, tr, st, ps.o, ps.dir);
+#if PTMI_PROBE == 2
+      ++pr_steps;
+      pr_sph += pt_ballot(tr.probe & 1) ? 1 : 0;
+      pr_oth += pt_ballot(tr.probe & 2) ? 1 : 0;
+      pr_node += pt_ballot(tr.probe & 4) ? 1 : 0;
+#endif
     }
+#if PTMI_PROBE == 2
+    {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      pr_trav += t - pr_t;
+      pr_t = t;
+    }
+#endif
     if (trav && !tr.busy()) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
@@ -378,6 +400,13 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
           }
         }
       }
+#if PTMI_PROBE == 2
+      {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        pr_shade += t - pr_t;
+        pr_t = t;
+      }
+#endif
       if (__ballot(live) == 0ull && drained && next >= wend) break;
     } else if (STAGED) {  // hand the wave's next items to the lanes without a path
       const unsigned long long want = __ballot(!live);
@@ -399,6 +428,16 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
       if (__ballot(live) == 0ull) break;
     }
   }
+#if PTMI_PROBE == 2
+  if (lane == 0) {
+    atomicAdd(&g_probe[8], pr_trav);
+    atomicAdd(&g_probe[9], pr_shade);
+    atomicAdd(&g_probe[10], pr_steps);
+    atomicAdd(&g_probe[11], pr_sph);
+    atomicAdd(&g_probe[12], pr_oth);
+    atomicAdd(&g_probe[13], pr_node);
+  }
+#endif
   if (!STAGED && ap) {
     ap[0] = acc.x;
     ap[1] = acc.y;
@@ -570,9 +609,9 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
 #if PTMI_PROBE
 extern "C" int ptmi_probe_read(unsigned long long* out, int reset) {
   hipDeviceSynchronize();
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi::g_probe), 8 * sizeof(unsigned long long));
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi::g_probe), 16 * sizeof(unsigned long long));
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {};
     hipMemcpyToSymbol(HIP_SYMBOL(ptmi::g_probe), z, sizeof(z));
   }
   return 0;
