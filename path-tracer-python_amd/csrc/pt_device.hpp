@@ -363,7 +363,9 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // faster (-0.5 %; profiles/r01/ab_fast_div_sqrt.log). One 80-B fetch per
 // popped entry, node or primitive, issued before the node/leaf branch (one
 // L2 wait per mixed step instead of two): -4.6 % mk, -14 % wf
-// (profiles/r01/ab_unified_fetch.log).
+// (profiles/r01/ab_unified_fetch.log). Node stride 128 B (one node per
+// line) -5 %; 64-B nodes with x/y centres computed +0.4 % (noise), kept at
+// 80 B (profiles/r01/ab_node_layout.log).
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
