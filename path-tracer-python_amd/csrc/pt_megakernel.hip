@@ -58,9 +58,21 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 }
 
 #ifndef PTMI_MK_SHADE_AT
-#define PTMI_MK_SHADE_AT 8  // shade once at most this many lanes are still mid-traversal (A/B: 8 > 16 > 24 > 0)
+#define PTMI_MK_SHADE_AT 12  // shade once at most this many lanes are still mid-traversal (A/B with the
+                             // traversal priority: 12 ~ 16 > 10 > 8 >> 4; without it 8 > 16 > 24 > 0)
 #endif
 
+#ifndef PTMI_MK_PRIO_TRAV
+// Wave priority (s_setprio) in the traversal loop and in shading: a wave in its
+// latency-bound traversal steps wins VALU issue over one in shading, so its
+// next node load goes out sooner (A/B with SHADE_AT 12: C2 +1.3 %, C4 +4 %,
+// C5 +1.4 %; the reverse order -1 %; profiles/r01/ab_prio_shade_at.log).
+// -1 = no s_setprio.
+#define PTMI_MK_PRIO_TRAV 1
+#endif
+#ifndef PTMI_MK_PRIO_SHADE
+#define PTMI_MK_PRIO_SHADE 0
+#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -227,6 +239,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   uint64_t pr_t = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
+#if PTMI_MK_PRIO_TRAV >= 0
+    __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
+#endif
     for (;;) {  // traversal steps
       // a lane's stack is empty unless its segment is mid-traversal (busy => trav)
       const unsigned long long mbusy = pt_ballot(tr.busy());
@@ -251,6 +266,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
       pr_trav += t - pr_t;
       pr_t = t;
     }
+#endif
+#if PTMI_MK_PRIO_TRAV >= 0
+    __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
     if (trav && !tr.busy()) {  // segment traced: shade it
       trav = false;
