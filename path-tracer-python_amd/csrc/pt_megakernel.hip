@@ -99,6 +99,8 @@ constexpr int kMkBlock = 64 * PTMI_MK_BLOCK_WAVES;
 #endif
 #ifndef PTMI_MK_TAIL_DIV
 #define PTMI_MK_TAIL_DIV 4  // a fetch takes at most (units left) / (TAIL_DIV * waves) units
+                            // (re-tuned: 2 is +3 % on C2 but -8 % on C4's long fog paths;
+                            // profiles/r01/ab_fetch_sizing.log)
 #endif
 // n / d for n < 2^26 by one 64-bit multiply: m = floor(2^(32+l) / d) + 1 with
 // 2^l >= d is exact because n * d < 2^(32+l) (items < 2^32, so units < 2^26).
