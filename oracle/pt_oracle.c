@@ -555,7 +555,8 @@ int or_render(const or_scene *sc, const or_frame *fr, int variant, float *accum,
               int x0, int y0, int w, int h, int s_begin, int s_count, int threads, or_stats *stats) {
     if (!sc || !fr || !accum || w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > fr->width || y0 + h > fr->height)
         return -1;
-    if (sc->num_bvh_nodes <= 0) return -2;
+    /* num_bvh_nodes == 0 (empty world, sah_bvh_builder.py:345-355) is legal: the root pop is
+       skipped as an invalid node (kernels.py:660) and every path misses */
     uint64_t seg = 0, med = 0, paths = 0;
     long npix = (long)w * (long)h;
 #ifdef _OPENMP

@@ -1,0 +1,90 @@
+"""GPU parity on edge cases the BASELINE scenes do not reach (through the
+C-ABI, against the CPU oracle, same bar as test_gpu_parity: per-pixel L-inf
+<= 1e-4 of accum/spp, and bit-exact in practice):
+
+* an empty scene and a one-sphere scene (the BVH root is a leaf);
+* linear BVHs 21, 28 and 51 levels deep, which select the 24-, 32- and
+  64-slot traversal kernels (the reference's 64-slot stack, kernels.py:719);
+* max_depth 1 and 2 (kernels.py:1139-1141 / 1383);
+* a zero-sample call, which must leave the accumulator untouched.
+"""
+import numpy as np
+import pytest
+
+from edge_scenes import edge_scene
+from parity_helpers import compare
+
+pytestmark = pytest.mark.gpu
+
+LINF_TOL = 1e-4
+
+
+def _oracle(sa, cam, bg, variant, spp, max_depth=50, seed=3):
+    import oracle
+    W, H = cam['width'], cam['height']
+    fr = oracle.make_frame(cam, bg, max_depth, seed, W, H)
+    acc = np.zeros((H, W, 3), np.float32)
+    oracle.render(oracle.OracleScene(sa), fr, variant, acc, (0, 0, W, H), 0, spp, 0)
+    return acc
+
+
+def _gpu(sa, cam, bg, variant, spp, max_depth=50, seed=3, acc=None):
+    import torch
+    from ptmi import device
+    W, H = cam['width'], cam['height']
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, max_depth, seed, W, H)
+    if acc is None:
+        acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
+    (integ.render_mk if variant == 'mk' else integ.render_wf)(fr, acc, 0, spp)
+    torch.cuda.synchronize()
+    return acc.cpu().numpy()
+
+
+def _check(name, variant, spp, max_depth=50):
+    sa, cam, bg = edge_scene(name)
+    ref = _oracle(sa, cam, bg, variant, spp, max_depth)
+    got = _gpu(sa, cam, bg, variant, spp, max_depth)
+    linf, exact = compare(got, ref, spp)
+    print(f'{name} {variant} spp={spp} max_depth={max_depth}: L-inf={linf:.3g} identical={exact:.5f}')
+    assert linf <= LINF_TOL
+    assert exact >= 0.999
+    return got
+
+
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_empty_scene_is_background(variant):
+    got = _check('empty', variant, 3)
+    bg = np.float32(3) * np.asarray(edge_scene('empty')[2], np.float32)
+    assert np.array_equal(got, np.broadcast_to(bg, got.shape))
+
+
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_single_primitive_root_leaf(variant):
+    got = _check('single', variant, 4)
+    assert not np.allclose(got, got[0, 0])  # the sphere is in view
+
+
+@pytest.mark.parametrize('name', ['chain22', 'chain29', 'chain52'])
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_deep_bvh_uses_wider_stacks(name, variant):
+    from ptmi import scene_data as sd
+    depth = sd.pack_device(edge_scene(name)[0]).max_leaf_depth
+    assert depth + 1 > 20  # beyond the 16/20-slot kernels
+    _check(name, variant, 4)
+
+
+@pytest.mark.parametrize('max_depth', [1, 2])
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_small_max_depth(variant, max_depth):
+    _check('chain22', variant, 4, max_depth)
+
+
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_zero_samples_leave_accumulator_untouched(variant):
+    import torch
+    sa, cam, bg = edge_scene('single')
+    W, H = cam['width'], cam['height']
+    acc = torch.full((H, W, 3), 0.25, dtype=torch.float32, device='cuda')
+    got = _gpu(sa, cam, bg, variant, 0, acc=acc)
+    assert np.all(got == np.float32(0.25))
