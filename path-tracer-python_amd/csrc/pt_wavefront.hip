@@ -500,12 +500,13 @@ __global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, 
 }
 
 namespace {
-int32_t* g_pinned_live = nullptr;  // host-pinned readback slots for the pipes' live-slot counts
+int32_t* g_pinned_live = nullptr;  // host-pinned readback slots [2][kPipes] for the pipes' live-slot counts
 
 // Library-owned streams and fork/join events for pipes 1.., per device.
 struct PipeStreams {
   hipStream_t s[kPipes] = {};
   hipEvent_t fork = nullptr, join[kPipes] = {};
+  hipEvent_t rb[2][kPipes] = {};  // live-count readbacks of two consecutive chunks
   bool ok = false;
 };
 PipeStreams g_pipes[64];
@@ -522,9 +523,17 @@ hipError_t pipe_streams(PipeStreams*& ps) {
     e = hipStreamCreateWithFlags(&ps->s[p], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ps->join[p], hipEventDisableTiming);
   }
+  for (int k = 0; k < 2; ++k)
+    for (int p = 0; p < kPipes && e == hipSuccess; ++p) e = hipEventCreateWithFlags(&ps->rb[k][p], hipEventDisableTiming);
   ps->ok = e == hipSuccess;
   return e;
 }
+#ifndef PTMI_WF_RB_CHUNK
+#define PTMI_WF_RB_CHUNK 8
+#endif
+#ifndef PTMI_WF_PIPELINED_RB
+#define PTMI_WF_PIPELINED_RB 1
+#endif
 #ifndef PTMI_WF_CAPACITY_LOG2
 #define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
 #endif
@@ -596,8 +605,16 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
   bool live[kPipes];
   for (int p = 0; p < kPipes; ++p) live[p] = true;
   int64_t it = 0;
-  const int32_t chunk = 8;  // iterations between live-count readbacks
+  const int32_t chunk = PTMI_WF_RB_CHUNK;  // iterations between live-count readbacks
   hipError_t err = hipSuccess;
+#if PTMI_WF_PIPELINED_RB
+  // The host reads chunk k's live counts only after chunk k + 1 is queued, so
+  // the pipes never idle through the readback's host round trip. Iterations
+  // on a drained pipe are no-ops (no slot holds or receives work), so the one
+  // extra chunk a pipe may run after draining changes nothing.
+  bool inflight[2][kPipes] = {};
+  int cur = 0;
+#endif
   while (it < max_iters) {
     const int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
@@ -617,6 +634,41 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     }
     it += n;
     err = hipGetLastError();
+#if PTMI_WF_PIPELINED_RB
+    for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
+      inflight[cur][p] = live[p];
+      if (!live[p]) continue;
+      err = hipMemcpyAsync(g_pinned_live + cur * kPipes + p, ctl_live(wbs[p]), sizeof(int32_t),
+                           hipMemcpyDeviceToHost, st[p]);
+      if (err == hipSuccess) err = hipEventRecord(ps.rb[cur][p], st[p]);
+    }
+    const int prev = cur ^ 1;
+    cur = prev;
+    bool waited = false;
+    for (int p = 0; p < kPipes && err == hipSuccess; ++p)
+      if (inflight[prev][p]) {
+        err = hipEventSynchronize(ps.rb[prev][p]);
+        waited = true;
+      }
+    if (err != hipSuccess) break;
+    if (!waited) continue;  // first chunk: nothing read back yet
+    bool any = false;
+    for (int p = 0; p < kPipes; ++p) {
+      if (inflight[prev][p]) live[p] = live[p] && g_pinned_live[prev * kPipes + p] != 0;
+      inflight[prev][p] = false;
+      any = any || live[p];
+    }
+    if (!any) break;
+  }
+  // the last chunk's readbacks may still be in flight: finish them before the
+  // pinned slots are reused
+  for (int k = 0; k < 2; ++k)
+    for (int p = 0; p < kPipes; ++p)
+      if (inflight[k][p]) {
+        hipError_t e = hipEventSynchronize(ps.rb[k][p]);
+        if (err == hipSuccess) err = e;
+      }
+#else
     for (int p = 0; p < kPipes && err == hipSuccess; ++p)
       if (live[p])
         err = hipMemcpyAsync(g_pinned_live + p, ctl_live(wbs[p]), sizeof(int32_t), hipMemcpyDeviceToHost, st[p]);
@@ -630,6 +682,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     }
     if (!any) break;
   }
+#endif
   for (int p = 1; p < kPipes; ++p) {  // join (also on error: the caller's stream must not run ahead)
     hipError_t e = hipEventRecord(ps.join[p], st[p]);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, ps.join[p], 0);
@@ -652,15 +705,13 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
   while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
   if (layout(npix, batch).total > ws_bytes) return hipErrorInvalidValue;
   if (!g_pinned_live) {
-    hipError_t e = hipHostMalloc((void**)&g_pinned_live, kPipes * sizeof(int32_t), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)&g_pinned_live, 2 * kPipes * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) return e;
   }
   PipeStreams* ps = nullptr;
-  if (kPipes > 1) {
-    hipError_t e = pipe_streams(ps);
+  {
+    hipError_t e = pipe_streams(ps);  // pipes 1.. streams, fork/join and readback events
     if (e != hipSuccess) return e;
-  } else {
-    ps = &g_pipes[0];
   }
   for (int32_t b0 = 0; b0 < s_count; b0 += batch) {
     const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
