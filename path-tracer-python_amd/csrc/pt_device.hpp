@@ -153,19 +153,8 @@ __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, f
   return false;
 }
 
-__device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o, pt_v3 d, float tmin,
-                                           float tmax, float& t) {  // kernels.py:311-362
-#if PTMI_LEAF_PRELOAD
-  // all 64 B in one round trip (the compiler otherwise sinks the loads into
-  // the branches: three dependent L2 round trips per quad test)
-  typedef float pt_f4 __attribute__((ext_vector_type(4)));
-  pt_f4 A = ((const pt_f4*)q)[0], B = ((const pt_f4*)q)[1], C = ((const pt_f4*)q)[2], E = ((const pt_f4*)q)[3];
-  asm volatile("" : "+v"(A), "+v"(B), "+v"(C), "+v"(E));
-  const float4 a = make_float4(A.x, A.y, A.z, A.w), b = make_float4(B.x, B.y, B.z, B.w);
-  const float4 c = make_float4(C.x, C.y, C.z, C.w), e = make_float4(E.x, E.y, E.z, E.w);
-#else
-  float4 a = q[0], b = q[1], c = q[2], e = q[3];
-#endif
+__device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const float4 c, const float4 e, pt_v3 o,
+                                           pt_v3 d, float tmin, float tmax, float& t) {  // kernels.py:311-362
   pt_v3 n = pt_v3f(a.x, a.y, a.z);
   float denom = pt_dot(n, d);
   if (fabsf(denom) >= 1e-8f) {
@@ -183,17 +172,23 @@ __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o
   return false;
 }
 
-__device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
-                                          float tmax, float& t) {  // kernels.py:252-307
+__device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o, pt_v3 d, float tmin,
+                                           float tmax, float& t) {
 #if PTMI_LEAF_PRELOAD
+  // all 64 B in one round trip (the compiler otherwise sinks the loads into
+  // the branches: three dependent L2 round trips per quad test)
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
-  pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1], C = ((const pt_f4*)tr)[2];
-  asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
-  const float4 a = make_float4(A.x, A.y, A.z, A.w), b = make_float4(B.x, B.y, B.z, B.w);
-  const float4 c = make_float4(C.x, C.y, C.z, C.w);
+  pt_f4 A = ((const pt_f4*)q)[0], B = ((const pt_f4*)q)[1], C = ((const pt_f4*)q)[2], E = ((const pt_f4*)q)[3];
+  asm volatile("" : "+v"(A), "+v"(B), "+v"(C), "+v"(E));
+  return hit_quad_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
+                    make_float4(C.x, C.y, C.z, C.w), make_float4(E.x, E.y, E.z, E.w), o, d, tmin, tmax, t);
 #else
-  float4 a = tr[0], b = tr[1], c = tr[2];
+  return hit_quad_v(q[0], q[1], q[2], q[3], o, d, tmin, tmax, t);
 #endif
+}
+
+__device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const float4 c, pt_v3 o, pt_v3 d,
+                                          float tmin, float tmax, float& t) {  // kernels.py:252-307
   pt_v3 v0 = pt_v3f(a.x, a.y, a.z), e1 = pt_v3f(a.w, b.x, b.y), e2 = pt_v3f(b.z, b.w, c.x);
   pt_v3 hv = pt_cross(d, e2);
   float det = pt_dot(e1, hv);
@@ -211,6 +206,19 @@ __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o
     }
   }
   return false;
+}
+
+__device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
+                                          float tmax, float& t) {
+#if PTMI_LEAF_PRELOAD
+  typedef float pt_f4 __attribute__((ext_vector_type(4)));
+  pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1], C = ((const pt_f4*)tr)[2];
+  asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
+  return hit_tri_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
+                   make_float4(C.x, C.y, C.z, C.w), o, d, tmin, tmax, t);
+#else
+  return hit_tri_v(tr[0], tr[1], tr[2], o, d, tmin, tmax, t);
+#endif
 }
 
 __device__ __forceinline__ bool hit_leaf(const DevScene& sc, int32_t ref, pt_v3 o, pt_v3 d, float tmin,
@@ -307,6 +315,12 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 __device__ unsigned long long g_probe[16];
 #endif
 
+#ifndef PTMI_EARLY_FETCH
+// A/B on MI355X (parity-identical): all of a step's loads issued before any
+// test, one wait per step: -4 % mk C2, -3 % mk C4, -1 % wf
+// (profiles/r01/ab_early_fetch.log)
+#define PTMI_EARLY_FETCH 0
+#endif
 #ifndef PTMI_NODE_CENTRES
 #define PTMI_NODE_CENTRES 1
 #endif
@@ -392,6 +406,46 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
 #endif
 #endif
   if (!(__uint_as_float(ent.y) <= tr.closest)) return;
+#if PTMI_EARLY_FETCH
+  // Every popping lane issues its own entry's load (80-B node, 16-B sphere,
+  // 64-B quad, 48-B triangle) into the same registers before any test runs,
+  // and the wave waits once: a step mixing node, sphere and quad lanes pays
+  // one L2 round trip instead of one per branch.
+  pt_f4 F0, F1, F2, F3, F4;
+  if (ref >= 0) {
+    gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);
+    F0 = nd[0]; F1 = nd[1]; F2 = nd[2]; F3 = nd[3]; F4 = nd[4];
+  } else {
+    const int32_t ty = leaf_type(ref), ix = leaf_index(ref);
+    if (ty == kSphere) {
+      F0 = ((const gf4*)sc.spheres)[ix];
+    } else if (ty == kQuad) {
+      gf4* q = (const gf4*)sc.quads + 4 * ix;
+      F0 = q[0]; F1 = q[1]; F2 = q[2]; F3 = q[3];
+    } else {
+      gf4* tq = (const gf4*)sc.tris + 3 * ix;
+      F0 = tq[0]; F1 = tq[1]; F2 = tq[2];
+    }
+  }
+  asm volatile("" : "+v"(F0), "+v"(F1), "+v"(F2), "+v"(F3), "+v"(F4));
+  if (ref < 0) {
+    const int32_t ty = leaf_type(ref);
+#if PTMI_PROBE == 2
+    tr.probe |= ty == kSphere ? 1 : 2;
+#endif
+    const float4 a = make_float4(F0.x, F0.y, F0.z, F0.w), b = make_float4(F1.x, F1.y, F1.z, F1.w);
+    const float4 c = make_float4(F2.x, F2.y, F2.z, F2.w), e = make_float4(F3.x, F3.y, F3.z, F3.w);
+    float t;  // leaf: kernels.py:671-697
+    const bool h = ty == kSphere ? hit_sphere_t(a, o, d, tr.tmin, tr.closest, t)
+                   : ty == kQuad ? hit_quad_v(a, b, c, e, o, d, tr.tmin, tr.closest, t)
+                                 : hit_tri_v(a, b, c, o, d, tr.tmin, tr.closest, t);
+    if (h && t < tr.closest) {
+      tr.closest = t;
+      tr.best = ref;
+    }
+    return;
+  }
+#else
   if (ref < 0) {
 #if PTMI_PROBE == 2
     tr.probe |= leaf_type(ref) == kSphere ? 1 : 2;
@@ -403,6 +457,7 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     }
     return;
   }
+#endif
 #if PTMI_PROBE == 2
   tr.probe |= 4;
 #endif
@@ -424,8 +479,12 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
   const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
   const float tmin = tr.tmin;
+#if PTMI_EARLY_FETCH
+  const pt_f4 A = F0, B = F1, C = F2, R = F3;
+#else
   gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // 80-B node at byte offset ref
   const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
+#endif
   const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
   const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
   const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
@@ -437,7 +496,11 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
   // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
 #if PTMI_NODE_CENTRES
+#if PTMI_EARLY_FETCH
+  const pt_f4 Cxy = F4;
+#else
   const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
+#endif
   const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
 #else
   const pt_f2 half = pt_f2s(0.5f);
