@@ -129,6 +129,12 @@ __device__ __forceinline__ void get_ray(const DevFrame& fr, int32_t px, int32_t 
 }
 
 // ---------------------------------------------------------------- primitives
+#ifndef PTMI_LEAF_FLAT
+// leaf tests as one predicate instead of nested early-outs (bit 1 quad +
+// triangle, bit 2 sphere). A/B on MI355X, parity-identical: bit 1 -1 % mk,
+// -2 % wf; bit 2 within noise (profiles/r01/ab_leaf_flat.log)
+#define PTMI_LEAF_FLAT 0
+#endif
 #ifndef PTMI_LEAF_PRELOAD
 #define PTMI_LEAF_PRELOAD 1  // A/B on MI355X: +1.4 % C2, +4 % C4, +2.6 % wavefront
 #endif
@@ -144,6 +150,15 @@ __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, f
   float h = pt_dot(d, oc);
   float cc = pt_dot(oc, oc) - s.w * s.w;
   float disc = h * h - a * cc;
+#if PTMI_LEAF_FLAT & 2
+  {  // no early-out on disc < 0: its NaN roots fail every range test
+    const float sq = sqrtf(disc);
+    float root = (h - sq) / a;
+    if (root < tmin || root > tmax) root = (h + sq) / a;
+    t = root;
+    return (disc >= 0.0f) & (root >= tmin) & (root <= tmax);
+  }
+#endif
   if (disc >= 0.0f) {
     float sq = sqrtf(disc);
     float root = (h - sq) / a;
@@ -157,6 +172,19 @@ __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const
                                            pt_v3 d, float tmin, float tmax, float& t) {  // kernels.py:311-362
   pt_v3 n = pt_v3f(a.x, a.y, a.z);
   float denom = pt_dot(n, d);
+#if PTMI_LEAF_FLAT & 1
+  {  // one predicate instead of nested early-outs (same values; a lane's t is used only on a hit)
+    const float tt = (a.w - pt_dot(n, o)) / denom;
+    const pt_v3 Q = pt_v3f(b.x, b.y, b.z), u = pt_v3f(b.w, c.x, c.y), v = pt_v3f(c.z, c.w, e.x);
+    const pt_v3 w = pt_v3f(e.y, e.z, e.w);
+    const pt_v3 pv = pt_sub(pt_add(o, pt_scale(d, tt)), Q);
+    const float alpha = pt_dot(w, pt_cross(pv, v));
+    const float beta = pt_dot(w, pt_cross(u, pv));
+    t = tt;
+    return (fabsf(denom) >= 1e-8f) & (tt >= tmin) & (tt <= tmax) & (alpha >= 0.0f) & (alpha <= 1.0f) &
+           (beta >= 0.0f) & (beta <= 1.0f);
+  }
+#endif
   if (fabsf(denom) >= 1e-8f) {
     float tt = (a.w - pt_dot(n, o)) / denom;
     if (tt >= tmin && tt <= tmax) {
@@ -192,6 +220,19 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
   pt_v3 v0 = pt_v3f(a.x, a.y, a.z), e1 = pt_v3f(a.w, b.x, b.y), e2 = pt_v3f(b.z, b.w, c.x);
   pt_v3 hv = pt_cross(d, e2);
   float det = pt_dot(e1, hv);
+#if PTMI_LEAF_FLAT & 1
+  {
+    const float inv = 1.0f / det;
+    const pt_v3 sv = pt_sub(o, v0);
+    const float u = inv * pt_dot(sv, hv);
+    const pt_v3 q = pt_cross(sv, e1);
+    const float v = inv * pt_dot(d, q);
+    const float tt = inv * pt_dot(e2, q);
+    t = tt;
+    return (fabsf(det) >= 1e-8f) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f) & (tt >= tmin) &
+           (tt <= tmax);
+  }
+#endif
   if (fabsf(det) >= 1e-8f) {
     float inv = 1.0f / det;
     pt_v3 s = pt_sub(o, v0);
