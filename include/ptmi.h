@@ -7,9 +7,9 @@
  * reference, so each entry point below names the reference launch/host site it
  * replaces. Plain C types only: device pointers are raw pointers owned by the
  * caller (the Python host allocates them as torch tensors); the library never
- * allocates device memory inside a render call (it owns one pinned readback
- * slot and, per device, the wavefront's 3 extra streams, created on first
- * use). All functions return 0 on success and a
+ * allocates device memory inside a render call (it owns a small pinned
+ * readback area and, per device, the wavefront's 3 extra streams and their
+ * events, created on first use). All functions return 0 on success and a
  * negative PTMI_E* code on error; ptmi_last_error() gives a message.
  */
 #ifndef PTMI_H
