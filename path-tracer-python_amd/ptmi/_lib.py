@@ -66,6 +66,17 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise PtmiError(f'libptmi.so not built ({path}); run `make -C path-tracer-python_amd/csrc` '
                         'or __graft_entry__.build()')
+    # One HIP runtime per process: torch's wheel carries its own libamdhip64
+    # (soname libamdhip64.so.7, the same as /opt/rocm's). Loaded after torch,
+    # libptmi binds to that copy; loaded first, it pulls in /opt/rocm's and
+    # torch then maps a second runtime, under which ptmi's launches find no
+    # device. So torch goes first whenever it is importable (the scene
+    # compiler reaches this loader for the native SAH builder before any
+    # device code runs).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     P = C.c_void_p
     lib.ptmi_version.restype = C.c_int

@@ -6,7 +6,8 @@ C-ABI, against the CPU oracle, same bar as test_gpu_parity: per-pixel L-inf
 * linear BVHs 21, 28 and 51 levels deep, which select the 24-, 32- and
   64-slot traversal kernels (the reference's 64-slot stack, kernels.py:719);
 * max_depth 1 and 2 (kernels.py:1139-1141 / 1383, SURVEY Q13/Q14);
-* a zero-sample call, which must leave the accumulator untouched.
+* a zero-sample call, which must leave the accumulator untouched;
+* 1x1, 3x1 and 13x7 frames (smaller than a wave or the pipes' work, ragged 8x8 squares).
 """
 import numpy as np
 import pytest
@@ -88,3 +89,44 @@ def test_zero_samples_leave_accumulator_untouched(variant):
     acc = torch.full((H, W, 3), 0.25, dtype=torch.float32, device='cuda')
     got = _gpu(sa, cam, bg, variant, 0, acc=acc)
     assert np.all(got == np.float32(0.25))
+
+
+@pytest.mark.parametrize('width', [1, 3, 13])
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_tiny_and_ragged_frames(variant, width):
+    """Frames far smaller than a wave, a tile or the wavefront's four pipes (most pipes get no
+    work and drain at once), and widths that are not multiples of the 8x8 work squares."""
+    sa, cam, bg = edge_scene('single', width)
+    W, H = cam['width'], cam['height']
+    ref = _oracle(sa, cam, bg, variant, 5)
+    got = _gpu(sa, cam, bg, variant, 5)
+    linf, exact = compare(got, ref, 5)
+    print(f'{W}x{H} {variant}: L-inf={linf:.3g} identical={exact:.5f}')
+    assert linf <= LINF_TOL
+    assert exact >= 0.999
+
+
+def test_library_loaded_before_torch_still_renders():
+    """Compiling a scene first loads libptmi (native SAH builder) before torch; the GPU path must
+    still work in that order (one HIP runtime per process, ptmi/_lib.py load())."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = '''
+import sys
+sys.path[:0] = [{pkg!r}, {tests!r}]
+from edge_scenes import edge_scene
+sa, cam, bg = edge_scene('single', 16)          # native SAH builder: libptmi loads here
+import torch
+from ptmi import device
+integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+fr = device.make_frame(cam, bg, 50, 3, cam['width'], cam['height'])
+acc = torch.zeros((cam['height'], cam['width'], 3), dtype=torch.float32, device='cuda')
+integ.render_mk(fr, acc, 0, 2)
+integ.render_wf(fr, acc, 2, 2)
+torch.cuda.synchronize()
+print('render ok', float(acc.sum()))
+'''.format(pkg=os.path.join(root, 'path-tracer-python_amd'), tests=os.path.join(root, 'tests'))
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and 'render ok' in r.stdout, r.stdout + r.stderr
