@@ -152,6 +152,21 @@ def cpu_baseline(sa, cam, bg, scene, variant, max_depth, seed, budget_s):
 TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'traffic.json')
 
 
+VALU_FILE = os.path.join(ROOT, 'profiles', 'valu.json')
+
+
+def valu_diagnostic(a, kernel):
+    """Secondary compute-side diagnostic of the dominant kernel
+    from the committed PMC passes (tools/pmc_valu.py), when collected on this
+    scene/integrator; None otherwise."""
+    try:
+        with open(VALU_FILE) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return rows.get(f'{a.scene}:{a.width}:{a.variant}:{kernel}')
+
+
 def measured_traffic(a, kernel):
     """HBM-side bytes per launch of ``kernel`` from the committed PMC summary
     (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE per dispatch, gfx950
@@ -296,6 +311,7 @@ def main():
             'timing': ('HIP events per launch on its stream, in the timed region' if inline else
                        'HIP events per launch on its stream, in a second pass over the same steps'),
         },
+        'valu_diagnostic': valu_diagnostic(a, dom),
         'kernels_ms': {k: round(v['ms'], 3) for k, v in prof.items() if v['launches']},
         'segments_per_sample': round(S, 4),
         'medium_traversals_per_sample': round(M, 4),

@@ -47,3 +47,8 @@ def test_every_preset_has_measured_traffic(preset, kernel):
 def test_algorithmic_bytes_cover_every_kernel_kind():
     assert set(bench.ALGO_BYTES) >= {'megakernel', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_generate',
                                      'wf_resolve', 'mk_resolve'}
+
+
+def test_valu_diagnostic_for_the_default_workload():
+    v = bench.valu_diagnostic(_args([]), 'megakernel')
+    assert v is not None and 0 < v['valu_issue_frac'] <= 1 and 0 < v['lane_efficiency'] <= 1

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""VALU-side diagnostic of the megakernel from the committed PMC passes
+(tools/gpu_pmc_latency.sh -> profiles/r01/pmc_latency/mk_{a,b,c}_counter_collection.csv),
+for SURVEY.md §8(d)'s "report VALU utilization as a secondary diagnostic".
+
+Per the largest mk_render_kernel dispatch of the run:
+  cycles          = GRBM_GUI_ACTIVE / 8            (the counter sums the 8 XCDs)
+  valu_issue_frac = 2 * SQ_INSTS_VALU / (1024 SIMDs * cycles)
+                    (MI355X_MICROARCH.md: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles)
+  lane_efficiency = SQ_THREAD_CYCLES_VALU / (64 * SQ_INSTS_VALU)
+  wait_frac       = SQ_WAIT_ANY / SQ_WAVE_CYCLES,  issue_frac = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
+Writes profiles/valu.json[KEY] (KEY = scene:width:variant:kernel, as bench.py looks it up).
+usage: pmc_valu.py [KEY] [DIR]"""
+import collections
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
+
+
+def main():
+    key = sys.argv[1] if len(sys.argv) > 1 else 'vol2_final_scene:800:mk:megakernel'
+    d = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, 'profiles', 'r01', 'pmc_latency')
+    per = collections.defaultdict(dict)
+    for p in 'abc':
+        with open(os.path.join(d, f'mk_{p}_counter_collection.csv')) as f:
+            for r in csv.DictReader(f):
+                if 'mk_render_kernel' in r['Kernel_Name']:
+                    c = per[(p, r['Dispatch_Id'])]
+                    c[r['Counter_Name']] = c.get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
+    v = {}
+    for p in 'abc':  # the largest dispatch of each pass (same launch in every pass)
+        runs = [c for (q, _), c in per.items() if q == p]
+        v.update(max(runs, key=lambda c: max(c.values())))
+    cycles = v['GRBM_GUI_ACTIVE'] / 8
+    out = {
+        'valu_issue_frac': round(2 * v['SQ_INSTS_VALU'] / (1024 * cycles), 4),
+        'lane_efficiency': round(v['SQ_THREAD_CYCLES_VALU'] / (64 * v['SQ_INSTS_VALU']), 4),
+        'wave_wait_frac': round(v['SQ_WAIT_ANY'] / v['SQ_WAVE_CYCLES'], 4),
+        'wave_issue_frac': round(v['SQ_ACTIVE_INST_ANY'] / v['SQ_WAVE_CYCLES'], 4),
+        'valu_insts': v['SQ_INSTS_VALU'],
+        'kernel_ms': round(cycles / 2.4e6, 3),
+        'source': 'profiles/r01/pmc_latency/mk_{a,b,c}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
+                  'tools/ab.py mk 32 1, one 32-spp launch); tools/pmc_valu.py',
+    }
+    path = os.path.join(ROOT, 'profiles', 'valu.json')
+    rows = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            rows = json.load(f)
+    rows[key] = out
+    with open(path, 'w') as f:
+        json.dump(rows, f, indent=1, sort_keys=True)
+    print(json.dumps({key: out}))
+
+
+if __name__ == '__main__':
+    main()
