@@ -30,6 +30,10 @@
 //   * PIPES: the queue is split into 4 independent parts, each looping
 //     intersect -> shade -> medium on its own stream, so the drain at the end
 //     of one pipe's launch is filled by another's (+21 % over one pipe).
+//   * The host learns that a pipe has drained from a 4-byte live count read
+//     back every 8 iterations, and waits for chunk k's counts only after
+//     chunk k + 1 is queued, so no pipe idles through the host round trip
+//     (the reference reads its ray count back every bounce, renderer.py:315).
 //   * Each ray carries its own wave count and is dropped at max_depth waves,
 //     exactly the reference's per-path budget (Q14, incl. passthrough Q11).
 //   * A path adds at most one colour to its pixel, when it ends (a miss, or an
