@@ -570,7 +570,7 @@ Layout layout(int32_t npix, int32_t batch) {
 }  // namespace
 
 #ifndef PTMI_WF_MAX_BLOCKS
-#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together
+#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together; A/B: 4096 -1.5 %, 8192 -3.5 % (C3)
 #endif
 static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must be a multiple of the shard count");
 
