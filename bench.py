@@ -23,7 +23,10 @@ Rank 0 at N=1 also times the CPU oracle (oracle/, a C restatement of the
 reference's kernels.py: the reference's ti.cpu path cannot run here, Taichi is
 absent) on a bounded slice of the same workload, and reports the dominant
 kernel's roofline from HIP events recorded around its launches in the timed
-region.
+region. `roofline.traffic` (PMC HBM-side bytes per launch, profiles/traffic.json)
+and `valu_diagnostic` (VALU issue share, lane efficiency and wave wait share of
+the dominant kernel, profiles/valu.json) come from committed rocprofv3 passes
+over the same workload (tools/pmc_traffic.py, tools/pmc_valu.py).
 """
 from __future__ import annotations
 
