@@ -94,6 +94,9 @@ constexpr int32_t kMissRef = 0x7fffffff;
 // driven through its own intersect/shade/medium loop on its own stream, so
 // one pipe's kernels fill the drain at the end of the other's. They share the
 // work pool (next-unit counters) and the staging buffer.
+#ifndef PTMI_WF_DEFER_NOISE
+#define PTMI_WF_DEFER_NOISE 1
+#endif
 #ifndef PTMI_WF_PIPES
 #define PTMI_WF_PIPES 4  // A/B on MI355X: 1 -> 2 pipes +15 % (C3), 2 -> 4 +5 %
 #endif
@@ -101,14 +104,17 @@ constexpr int32_t kPipes = PTMI_WF_PIPES;
 
 // Device-scope atomics are performed per cache line at the memory side, so
 // counters sharing a line serialize as one: every counter gets its own
-// 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 9 lines:
-// medium-queue count per shard, live slots (read by the host).
+// 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 17 lines:
+// medium-queue count per shard, live slots (read by the host), deferred-
+// shading count per shard.
 constexpr int32_t kLine = 64;
-constexpr int32_t kPipeLines = 9;
+constexpr int32_t kPipeLines = 17;
 constexpr int32_t kCtlWords = (8 + kPipeLines * kPipes) * kLine;
 __host__ __device__ __forceinline__ int32_t* ctl_medium(const WfBufs& wb, int32_t s) { return wb.ctl + s * kLine; }
 __host__ __device__ __forceinline__ int32_t* ctl_next(const WfBufs& wb, int32_t s) { return wb.next + s * kLine; }
 __host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl + 8 * kLine; }
+// deferred-shading (Perlin-textured surface hits) count per shard: lines 9-16
+__host__ __device__ __forceinline__ int32_t* ctl_noise(const WfBufs& wb, int32_t s) { return wb.ctl + (9 + s) * kLine; }
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -321,7 +327,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
-  if (blockIdx.x < kShards && tid == 0) *ctl_medium(wb, blockIdx.x) = 0;  // medium counts of this iteration
+  if (blockIdx.x < kShards && tid == 0) {  // medium and deferred-shading counts of this iteration
+    *ctl_medium(wb, blockIdx.x) = 0;
+    *ctl_noise(wb, blockIdx.x) = 0;
+  }
   const Queue q = wb.q;
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_live = 0;
@@ -372,6 +381,36 @@ __device__ __forceinline__ void finish_lane(const WfBufs& wb, int32_t i, bool en
   if (ended) reinterpret_cast<uint32_t*>(wb.q.c + i)[1] = kPending;
 }
 
+// Surface branch of shade_and_scatter (kernels.py:1359-1399) for slot ray
+// `ray` whose closest hit (t, ref) has material g.
+__device__ __forceinline__ void shade_surface(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
+                                              const Ray& ray, float t, int32_t ref, int32_t g, bool& ended,
+                                              bool& go, Ray& cont) {
+  Item it = decode_item(fr, wb, ray.item);
+  Rng r{path_key(fr, wb, it), ray.ctr};
+  const Mat m = load_mat(sc, g);
+  pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, t));
+  pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
+  pt_v3 emit = emitted(m);
+  pt_v3 sdir, att;
+  bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
+  go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
+  if (!go) {
+    ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
+    stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
+                                                                          : pt_v3f(0.0f, 0.0f, 0.0f));
+  }
+}
+
+// Surface hits whose scatter evaluates Perlin turbulence (a noise texture on
+// a Lambertian or isotropic material, kernels.py:1013-1015): deferred to a
+// compacted list shaded by wf_medium, so one such lane no longer puts three
+// octaves of table round trips into every wave of wf_shade that holds it.
+__device__ __forceinline__ bool noise_shaded(uint32_t flags) {
+  const uint32_t mt = flags & 0xfu, tx = (flags >> 4) & 0xfu;
+  return tx == 3u && (mt == 0u || mt == 4u);
+}
+
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
 // medium-boundary hits go to their shard's medium queue segment.
 __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
@@ -384,7 +423,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
   uint32_t n_ended = 0;
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < wb.capacity; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
-    bool to_medium = false, ended = false, go = false;
+    bool to_medium = false, to_noise = false, ended = false, go = false;
     Ray cont;
     const bool live = i < wb.capacity && slot_item(q, i) < kPending;
     if (live) {
@@ -396,28 +435,24 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
         ended = true;
       } else {
         const int32_t g = mat_index(sc, ref);
-        if ((mat_flags(sc, g) >> 8) & 1u) {
+        const uint32_t fl = mat_flags(sc, g);
+        if ((fl >> 8) & 1u) {
           to_medium = true;
+        } else if (PTMI_WF_DEFER_NOISE && noise_shaded(fl)) {
+          to_noise = true;
         } else {
-          Item it = decode_item(fr, wb, ray.item);
-          Rng r{path_key(fr, wb, it), ray.ctr};
-          const Mat m = load_mat(sc, g);
-          pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
-          pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
-          pt_v3 emit = emitted(m);
-          pt_v3 sdir, att;
-          bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
-          go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
-          if (!go) {
-            ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
-            stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
-                                                                                  : pt_v3f(0.0f, 0.0f, 0.0f));
-          }
+          shade_surface(sc, fr, wb, ray, h.x, ref, g, ended, go, cont);
         }
       }
     }
     const int32_t mslot = wave_ticket(to_medium, ctl_medium(wb, shard));
     if (to_medium) wb.medq[shard * wb.medseg + mslot] = i;
+#if PTMI_WF_DEFER_NOISE
+    // deferred hits fill the shard's segment from the top; a slot is in at
+    // most one of the two lists, so together they never exceed the segment
+    const int32_t nslot = wave_ticket(to_noise, ctl_noise(wb, shard));
+    if (to_noise) wb.medq[shard * wb.medseg + wb.medseg - 1 - nslot] = i;
+#endif
     finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
@@ -428,7 +463,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
 // kernels.py:365-450) and the volume branch of shade_and_scatter
 // (kernels.py:1326-1357). Work index j runs over the concatenated shard segments.
 template <int STACK>
-__global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
+#ifndef PTMI_WF_MEDIUM_MIN_WAVES
+#define PTMI_WF_MEDIUM_MIN_WAVES 4  // <= 128 VGPRs: with the deferred shading list it needs 131 otherwise (3 waves/SIMD)
+#endif
+__global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
                                                     unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
@@ -440,13 +478,38 @@ __global__ __launch_bounds__(kWfBlock) void wf_medium(DevScene sc, DevFrame fr, 
     n += cnt[s];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
+  int32_t nn = 0;  // deferred surface hits (wf_shade), after the medium rays in the index space
+#if PTMI_WF_DEFER_NOISE
+  int32_t cntn[kShards];
+#pragma unroll
+  for (int s = 0; s < kShards; ++s) {
+    cntn[s] = __builtin_amdgcn_readfirstlane(*ctl_noise(wb, s));
+    nn += cntn[s];
+  }
+#endif
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0;
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
     Ray cont;
     int32_t i = -1, shard = 0;
+#if PTMI_WF_DEFER_NOISE
+    if (j >= n && j < n + nn) {
+      int32_t off = j - n;
+#pragma unroll
+      for (int s = 0; s + 1 < kShards; ++s) {
+        if (shard == s && off >= cntn[s]) {
+          off -= cntn[s];
+          shard = s + 1;
+        }
+      }
+      i = wb.medq[shard * wb.medseg + wb.medseg - 1 - off];
+      const float2 h = wb.hit[i];
+      const int32_t ref = __float_as_int(h.y);
+      shade_surface(sc, fr, wb, load_ray(wb.q, i), h.x, ref, mat_index(sc, ref), ended, go, cont);
+    }
+#endif
     if (j < n) {
       int32_t off = j;
 #pragma unroll
