@@ -73,6 +73,9 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_PRIO_SHADE
 #define PTMI_MK_PRIO_SHADE 0
 #endif
+#ifndef PTMI_MK_HOLD_NOISE
+#define PTMI_MK_HOLD_NOISE 0  // A/B: 4 or 8 held lanes -1 to -1.5 % (profiles/r01/ab_mk_hold_noise.log)
+#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   Trav tr;
   tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
+  bool hold = false;  // PTMI_MK_HOLD_NOISE: a traced Perlin-textured hit waiting for more of its kind
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
     trav_begin<STACK, kMkBlock>(sc, tr, st, ps.dir, ps.o, em ? ps.t_entry + 0.0001f : kTMin, kTMax);  // :418/:1057
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
+      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy() && !hold) != 0ull) break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -272,7 +276,21 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
 #if PTMI_MK_PRIO_TRAV >= 0
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
-    if (trav && !tr.busy()) {  // segment traced: shade it
+#if PTMI_MK_HOLD_NOISE
+    {  // Perlin-textured surface hits wait (lane idle) until PTMI_MK_HOLD_NOISE of them are
+       // ready or no lane is still traversing, so the wave pays the turbulence's table round
+       // trips once for several lanes (A/B knob)
+      bool nr = false;
+      if (trav && !tr.busy() && ps.mode != kModeMediumExit && tr.any()) {
+        const uint32_t fl = mat_flags(sc, mat_index(sc, tr.best));
+        nr = ((fl >> 4) & 0xfu) == 3u && ((fl & 0xfu) == 0u || (fl & 0xfu) == 4u) && !((fl >> 8) & 1u);
+      }
+      const unsigned long long mn = pt_ballot(nr);
+      const uint32_t nn = __builtin_popcount((uint32_t)mn) + __builtin_popcount((uint32_t)(mn >> 32));
+      hold = nr && nn < (uint32_t)PTMI_MK_HOLD_NOISE && pt_ballot(tr.busy()) != 0ull;
+    }
+#endif
+    if (trav && !tr.busy() && !hold) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
       const bool hit = tr.any();
