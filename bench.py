@@ -327,7 +327,8 @@ def main():
     if rank == 0:
         if a.save_image:
             from PIL import Image
-            img = integ.tonemap(acc, sps * a.steps * world).cpu().numpy()
+            # tiles: every pixel has sps * steps samples; samples: each rank added its own
+            img = integ.tonemap(acc, sps * a.steps * (world if a.shard == "samples" else 1)).cpu().numpy()
             Image.fromarray(img).save(a.save_image)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -125,7 +125,9 @@ int ptmi_mk_render(const ptmi_scene_view *scene, const ptmi_frame *frame, float 
  * until the batch is done, so a launch has no partly occupied last round.
  * Each path's colour goes to a staging slot [sample][pixel] of `workspace`
  * and a resolve kernel adds them into accum in sample order: same results,
- * bit for bit, as ptmi_mk_render. workspace: device memory (16-byte aligned)
+ * bit for bit, as ptmi_mk_render. A batch holds fewer than 2^32 (8x8 tile,
+ * sample, pixel) item ids: larger calls run as several batches.
+ * workspace: device memory (16-byte aligned)
  * of at least ptmi_mk_workspace_bytes(frame, 1) bytes;
  * ptmi_mk_workspace_bytes(frame, B) = 12 * pixels * B (rounded up to 256) +
  * 256 lets one batch hold B samples. Asynchronous, graph-capturable. */
@@ -147,7 +149,12 @@ int ptmi_mk_render_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, voi
  * joined back into it with events, so the work is ordered after earlier and
  * before later work on `stream` like one launch. Synchronises the pipes once
  * every few queue iterations to read their live-ray counts (not
- * graph-capturable). */
+ * graph-capturable). Thread-safe: the library's per-device streams, events
+ * and pinned readback slots are created under a per-device lock, and calls on
+ * one device are serialised by that lock (calls on different devices run
+ * concurrently). Launches go to the current HIP device, which must be the
+ * device holding the pointers. Batches are capped at 2^31 - 1 (sample,
+ * pixel) work items whatever the workspace size. */
 size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,

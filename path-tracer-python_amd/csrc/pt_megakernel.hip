@@ -626,6 +626,10 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
     return mk_render(sc, fr, stack_needed, accum, s_begin, s_count, counters, stream);
   const int32_t npix = fr.w * fr.n_rows;
   int32_t batch = s_count;
+  // item ids (tile, sample, pixel of the 8x8 tile) are 32-bit: tiles * batch * 64 < 2^32
+  const int64_t max_batch = ((1ll << 32) - 1) / (tiles * 64);
+  if (max_batch < 1) return hipErrorInvalidValue;
+  if (batch > max_batch) batch = (int32_t)max_batch;
   while (batch > 1 && mk_workspace_bytes(npix, batch) > ws_bytes) batch = (batch + 1) / 2;
   if (mk_workspace_bytes(npix, batch) > ws_bytes) return hipErrorInvalidValue;
   for (int32_t b0 = 0; b0 < s_count; b0 += batch) {

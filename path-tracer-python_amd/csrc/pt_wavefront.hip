@@ -46,6 +46,8 @@
 #include "pt_launch.hpp"
 #include "pt_prof.hpp"
 
+#include <mutex>
+
 namespace ptmi {
 
 constexpr int kShards = 8;
@@ -567,31 +569,36 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
 }
 
 namespace {
-int32_t* g_pinned_live = nullptr;  // host-pinned readback slots [2][kPipes] for the pipes' live-slot counts
-
-// Library-owned streams and fork/join events for pipes 1.., per device.
+// Library-owned state of one device, created on first use: the streams and
+// fork/join events of pipes 1.., the live-count readback events and their
+// host-pinned slots [2][kPipes]. `mu` serialises ptmi_wf_render calls on the
+// device (each call drives all pipes and reads their counts back), so two
+// host threads rendering on one device never share readback slots; calls on
+// different devices run concurrently.
 struct PipeStreams {
+  std::mutex mu;
   hipStream_t s[kPipes] = {};
   hipEvent_t fork = nullptr, join[kPipes] = {};
   hipEvent_t rb[2][kPipes] = {};  // live-count readbacks of two consecutive chunks
+  int32_t* pinned_live = nullptr;
   bool ok = false;
 };
-PipeStreams g_pipes[64];
+constexpr int kMaxDevices = 64;
+PipeStreams g_pipes[kMaxDevices];
 
-hipError_t pipe_streams(PipeStreams*& ps) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  ps = &g_pipes[dev];
+// Called with ps->mu held.
+hipError_t pipe_streams_init(PipeStreams* ps) {
   if (ps->ok) return hipSuccess;
-  e = hipEventCreateWithFlags(&ps->fork, hipEventDisableTiming);
+  hipError_t e = hipSuccess;
+  if (!ps->pinned_live) e = hipHostMalloc((void**)&ps->pinned_live, 2 * kPipes * sizeof(int32_t), hipHostMallocDefault);
+  if (e == hipSuccess && !ps->fork) e = hipEventCreateWithFlags(&ps->fork, hipEventDisableTiming);
   for (int p = 1; p < kPipes && e == hipSuccess; ++p) {
-    e = hipStreamCreateWithFlags(&ps->s[p], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ps->join[p], hipEventDisableTiming);
+    if (!ps->s[p]) e = hipStreamCreateWithFlags(&ps->s[p], hipStreamNonBlocking);
+    if (e == hipSuccess && !ps->join[p]) e = hipEventCreateWithFlags(&ps->join[p], hipEventDisableTiming);
   }
   for (int k = 0; k < 2; ++k)
-    for (int p = 0; p < kPipes && e == hipSuccess; ++p) e = hipEventCreateWithFlags(&ps->rb[k][p], hipEventDisableTiming);
+    for (int p = 0; p < kPipes && e == hipSuccess; ++p)
+      if (!ps->rb[k][p]) e = hipEventCreateWithFlags(&ps->rb[k][p], hipEventDisableTiming);
   ps->ok = e == hipSuccess;
   return e;
 }
@@ -705,7 +712,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
       inflight[cur][p] = live[p];
       if (!live[p]) continue;
-      err = hipMemcpyAsync(g_pinned_live + cur * kPipes + p, ctl_live(wbs[p]), sizeof(int32_t),
+      err = hipMemcpyAsync(ps.pinned_live + cur * kPipes + p, ctl_live(wbs[p]), sizeof(int32_t),
                            hipMemcpyDeviceToHost, st[p]);
       if (err == hipSuccess) err = hipEventRecord(ps.rb[cur][p], st[p]);
     }
@@ -721,7 +728,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     if (!waited) continue;  // first chunk: nothing read back yet
     bool any = false;
     for (int p = 0; p < kPipes; ++p) {
-      if (inflight[prev][p]) live[p] = live[p] && g_pinned_live[prev * kPipes + p] != 0;
+      if (inflight[prev][p]) live[p] = live[p] && ps.pinned_live[prev * kPipes + p] != 0;
       inflight[prev][p] = false;
       any = any || live[p];
     }
@@ -738,13 +745,13 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
 #else
     for (int p = 0; p < kPipes && err == hipSuccess; ++p)
       if (live[p])
-        err = hipMemcpyAsync(g_pinned_live + p, ctl_live(wbs[p]), sizeof(int32_t), hipMemcpyDeviceToHost, st[p]);
+        err = hipMemcpyAsync(ps.pinned_live + p, ctl_live(wbs[p]), sizeof(int32_t), hipMemcpyDeviceToHost, st[p]);
     for (int p = 0; p < kPipes && err == hipSuccess; ++p)
       if (live[p]) err = hipStreamSynchronize(st[p]);
     if (err != hipSuccess) break;
     bool any = false;
     for (int p = 0; p < kPipes; ++p) {
-      live[p] = live[p] && g_pinned_live[p] != 0;
+      live[p] = live[p] && ps.pinned_live[p] != 0;
       any = any || live[p];
     }
     if (!any) break;
@@ -768,16 +775,22 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
                      float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
                      hipStream_t stream) {
   const int32_t npix = fr.w * fr.n_rows;
+  // work items (sample, pixel) of a batch are 32-bit ids: at most 2^31 - 1
   int32_t batch = s_count;
+  if ((int64_t)npix * batch > 0x7fffffffll) batch = (int32_t)(0x7fffffffll / npix);
+  if (batch < 1) return hipErrorInvalidValue;
   while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
   if (layout(npix, batch).total > ws_bytes) return hipErrorInvalidValue;
-  if (!g_pinned_live) {
-    hipError_t e = hipHostMalloc((void**)&g_pinned_live, 2 * kPipes * sizeof(int32_t), hipHostMallocDefault);
-    if (e != hipSuccess) return e;
-  }
-  PipeStreams* ps = nullptr;
+  int dev = 0;
   {
-    hipError_t e = pipe_streams(ps);  // pipes 1.. streams, fork/join and readback events
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  }
+  PipeStreams* ps = &g_pipes[dev];
+  std::lock_guard<std::mutex> lock(ps->mu);
+  {
+    hipError_t e = pipe_streams_init(ps);  // pipes 1.. streams, fork/join and readback events, pinned slots
     if (e != hipSuccess) return e;
   }
   for (int32_t b0 = 0; b0 < s_count; b0 += batch) {

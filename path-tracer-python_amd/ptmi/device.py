@@ -17,9 +17,11 @@ from . import _lib
 from .scene_data import DeviceLayout, SceneArrays, camera_upload, pack_device
 
 
-def _stream_ptr(stream=None):
+def _stream_ptr(stream=None, device=None):
     if stream is None:
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(device)
+    elif device is not None and stream.device != device:
+        raise _lib.PtmiError(f'stream is on {stream.device}, the scene on {device}')
     return C.c_void_p(stream.cuda_stream)
 
 
@@ -36,7 +38,13 @@ class DeviceScene:
         require_gpu()
         layout = scene if isinstance(scene, DeviceLayout) else pack_device(scene)
         self.layout = layout
-        self.device = torch.device(device if device is not None else 'cuda')
+        dev = torch.device(device if device is not None else 'cuda')
+        if dev.type != 'cuda':
+            raise _lib.PtmiError(f'DeviceScene needs a cuda device, got {dev}')
+        # a bare 'cuda' means the current device; fixed here so every later
+        # launch goes to the device that holds the scene (the C-ABI launches on
+        # the current HIP device)
+        self.device = torch.device('cuda', dev.index if dev.index is not None else torch.cuda.current_device())
 
         def up(a):
             a = np.ascontiguousarray(a)
@@ -126,24 +134,34 @@ class Integrator:
     def _cnt(self):
         return C.c_void_p(self.counters.data_ptr()) if self.counters is not None else None
 
+    def _dev(self):
+        """Context that makes the scene's device current for a C-ABI call."""
+        return torch.cuda.device(self.scene.device)
+
+    def _stream(self, stream):
+        return _stream_ptr(stream, self.scene.device)
+
     # multi-sample megakernel calls run as (tile, sample chunk) work units with
     # staged colours (ptmi_mk_render_ws); single samples accumulate directly
     MK_STAGED_MIN_SAMPLES = 2
 
     def render_mk(self, frame, accum, sample_begin, sample_count, stream=None, staged=None):
-        _check_accum(accum, frame)
+        _check_accum(accum, frame, self.scene.device)
         if staged is None:
             staged = int(sample_count) >= self.MK_STAGED_MIN_SAMPLES
-        if staged:
-            ws = self.workspace(frame, sample_count, 'mk')
-            _lib.check(self.lib.ptmi_mk_render_ws(C.byref(self.scene.view), C.byref(frame), C.c_void_p(ws.data_ptr()),
-                                                  self._ws_bytes, C.c_void_p(accum.data_ptr()), int(sample_begin),
-                                                  int(sample_count), self._cnt(), _stream_ptr(stream)),
-                       'ptmi_mk_render_ws')
-            return
-        _lib.check(self.lib.ptmi_mk_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(accum.data_ptr()),
-                                           int(sample_begin), int(sample_count), self._cnt(), _stream_ptr(stream)),
-                   'ptmi_mk_render')
+        with self._dev():
+            if staged:
+                ws = self.workspace(frame, sample_count, 'mk')
+                _lib.check(self.lib.ptmi_mk_render_ws(C.byref(self.scene.view), C.byref(frame),
+                                                      C.c_void_p(ws.data_ptr()), self._ws_bytes,
+                                                      C.c_void_p(accum.data_ptr()), int(sample_begin),
+                                                      int(sample_count), self._cnt(), self._stream(stream)),
+                           'ptmi_mk_render_ws')
+                return
+            _lib.check(self.lib.ptmi_mk_render(C.byref(self.scene.view), C.byref(frame),
+                                               C.c_void_p(accum.data_ptr()), int(sample_begin), int(sample_count),
+                                               self._cnt(), self._stream(stream)),
+                       'ptmi_mk_render')
 
     # staging budget for the per-(sample, pixel) colour slots of one batch
     STAGING_BYTES = 1 << 30
@@ -164,23 +182,28 @@ class Integrator:
         return self._ws
 
     def render_wf(self, frame, accum, sample_begin, sample_count, stream=None):
-        _check_accum(accum, frame)
-        ws = self.workspace(frame, sample_count)
-        _lib.check(self.lib.ptmi_wf_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(ws.data_ptr()),
-                                           self._ws_bytes, C.c_void_p(accum.data_ptr()), int(sample_begin),
-                                           int(sample_count), self._cnt(), _stream_ptr(stream)),
-                   'ptmi_wf_render')
+        _check_accum(accum, frame, self.scene.device)
+        with self._dev():
+            ws = self.workspace(frame, sample_count)
+            _lib.check(self.lib.ptmi_wf_render(C.byref(self.scene.view), C.byref(frame), C.c_void_p(ws.data_ptr()),
+                                               self._ws_bytes, C.c_void_p(accum.data_ptr()), int(sample_begin),
+                                               int(sample_count), self._cnt(), self._stream(stream)),
+                       'ptmi_wf_render')
 
     def clear(self, frame, accum, stream=None):
-        _check_accum(accum, frame)
-        _lib.check(self.lib.ptmi_clear(C.byref(frame), C.c_void_p(accum.data_ptr()), _stream_ptr(stream)),
-                   'ptmi_clear')
+        _check_accum(accum, frame, self.scene.device)
+        with self._dev():
+            _lib.check(self.lib.ptmi_clear(C.byref(frame), C.c_void_p(accum.data_ptr()), self._stream(stream)),
+                       'ptmi_clear')
 
     def tonemap(self, accum, spp, stream=None):
+        if accum.device != self.scene.device:
+            raise _lib.PtmiError(f'accum is on {accum.device}, the scene on {self.scene.device}')
         h, w, _ = accum.shape
-        out = torch.empty((h, w, 3), dtype=torch.uint8, device=accum.device)
-        _lib.check(self.lib.ptmi_tonemap(C.c_void_p(accum.data_ptr()), C.c_void_p(out.data_ptr()), w, h, int(spp),
-                                         _stream_ptr(stream)), 'ptmi_tonemap')
+        with self._dev():
+            out = torch.empty((h, w, 3), dtype=torch.uint8, device=accum.device)
+            _lib.check(self.lib.ptmi_tonemap(C.c_void_p(accum.data_ptr()), C.c_void_p(out.data_ptr()), w, h,
+                                             int(spp), self._stream(stream)), 'ptmi_tonemap')
         return out
 
     def read_counters(self):
@@ -194,8 +217,10 @@ class Integrator:
             self.counters.zero_()
 
 
-def _check_accum(accum, frame):
+def _check_accum(accum, frame, device=None):
     if not (isinstance(accum, torch.Tensor) and accum.is_cuda and accum.dtype == torch.float32
             and accum.is_contiguous() and tuple(accum.shape) == (frame.height, frame.width, 3)):
         raise _lib.PtmiError(f'accum must be a contiguous cuda float32 tensor of shape '
                              f'({frame.height}, {frame.width}, 3)')
+    if device is not None and accum.device != device:
+        raise _lib.PtmiError(f'accum is on {accum.device}, the scene on {device}')

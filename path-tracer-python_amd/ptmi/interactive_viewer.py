@@ -133,7 +133,7 @@ class InteractiveViewer(MI355XRenderer):
         self._upload_camera_to_gpu()
         t0 = time.time()
         self.render_sample(0)  # warm-up sample, cleared (interactive_viewer.py:355-359)
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(self.dscene.device)
         self.clear_accumulation_buffer()
         self.integrator.reset_counters()
         print(f'  Kernel Warmup: {(time.time() - t0) * 1000:6.2f}ms')
@@ -148,7 +148,7 @@ class InteractiveViewer(MI355XRenderer):
                 n = 1  # the reference prints sample 1
             t = time.time()
             self.integrator.render_mk(self.frame, self.accum, self.current_sample, n)
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(self.dscene.device)
             dt = (time.time() - t) / n
             self.sample_times += [dt] * n
             self.current_sample += n

@@ -99,10 +99,10 @@ class MI355XRenderer:
         spp = int(self.cam.samples_per_pixel)
         t0 = time.time()
         render_fn(self.frame, self.accum, 0, 1)  # warm-up sample, then cleared (renderer.py:381-385)
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(self.dscene.device)
         self.clear_accumulation_buffer()
         self.integrator.reset_counters()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(self.dscene.device)
         self.timing['kernel_warmup'] = time.time() - t0
         print(f'\n{self.__class__.__name__} ({label})')
         print(f'Resolution: {self.cam.img_width}x{self.cam.img_height} | Samples: {spp} | Depth: {self.max_depth}')
@@ -114,7 +114,7 @@ class MI355XRenderer:
             n = min(per, spp - done)
             t = time.time()
             render_fn(self.frame, self.accum, done, n)
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(self.dscene.device)
             dt = time.time() - t
             self.sample_times += [dt / n] * n
             done += n

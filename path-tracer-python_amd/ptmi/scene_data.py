@@ -238,9 +238,19 @@ def _pack_mats(m, n):
 
 
 def leaf_depths(bvh):
-    """Depth of every node (root = 0) of a preorder flattened BVH."""
+    """Depth of every node (root = 0) of a preorder flattened BVH.
+
+    The depths size the kernels' traversal stack, which has no overflow check,
+    so a BVH whose children do not follow their parent (not the preorder
+    flatten() of sah_bvh_builder.py:338-418 writes) is refused here rather
+    than reported with too small a depth."""
     left, right = bvh['bvh_left_child'], bvh['bvh_right_child']
     n = left.shape[0]
+    idx = np.arange(n)
+    for name, ch in (('left', left), ('right', right)):
+        has = ch >= 0
+        if np.any(ch[has] >= n) or np.any(ch[has] <= idx[has]):
+            raise ValueError(f'BVH is not in preorder: a {name} child does not follow its parent')
     depth = np.zeros(n, np.int32)
     for i in range(n):  # preorder: parents precede children
         if left[i] >= 0:

@@ -1,0 +1,123 @@
+"""GPU tests of the host-side state around the C-ABI (through the C-ABI, on
+the box's GPU):
+
+* two host threads calling ptmi_wf_render on one device at once: each call
+  drives all pipes and reads their live counts back, so the per-device
+  readback slots must not be shared between calls (a call whose pipe read
+  another call's 0 would stop early and drop samples without an error);
+* the device a DeviceScene is bound to decides where its launches go, not
+  whichever device happens to be current;
+* a staged megakernel call whose (tile, sample, pixel) item ids would pass
+  2^32 is split into batches instead of failing.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from parity_helpers import scene_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame_acc(cam, win, seed=5):
+    import torch
+    from ptmi import device
+    W, H = cam['width'], cam['height']
+    fr = device.make_frame(cam, (0.0, 0.0, 0.0), 50, seed, W, H, win)
+    return fr, torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
+
+
+def test_wf_render_concurrent_threads_one_device():
+    import torch
+    from ptmi import device
+    sa, cam, _ = scene_inputs('vol2_final_scene', 800)
+    win, spp = (352, 352, 96, 96), 6
+    dscene = device.DeviceScene.from_arrays(sa)
+    n = 3
+    integs = [device.Integrator(dscene) for _ in range(n)]
+    accs = [_frame_acc(cam, win) for _ in range(n)]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    errors = []
+    start = threading.Barrier(n)
+
+    def work(k):
+        try:
+            fr_k, acc_k = accs[k]
+            with torch.cuda.stream(streams[k]):
+                start.wait()
+                for rep in range(2):  # two calls per thread: overlapping starts and ends
+                    integs[k].render_wf(fr_k, acc_k, rep * spp, spp, stream=streams[k])
+            streams[k].synchronize()
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(n)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    # each thread made two calls (samples 0..spp-1, then spp..2spp-1): compare
+    # with the same two calls made from this thread alone
+    ref_integ = device.Integrator(dscene)
+    fr2, ref2 = _frame_acc(cam, win)
+    ref_integ.render_wf(fr2, ref2, 0, spp)
+    ref_integ.render_wf(fr2, ref2, spp, spp)
+    torch.cuda.synchronize()
+    ref2 = ref2.cpu().numpy()
+    assert ref2.sum() > 0
+    for k in range(n):
+        got = accs[k][1].cpu().numpy()
+        assert np.array_equal(got, ref2), f'thread {k}: differs from the single-threaded render'
+        paths = integs[k].read_counters()['paths']
+        assert paths == 2 * spp * win[2] * win[3], f'thread {k}: {paths} paths'
+
+
+def test_scene_device_is_fixed_at_construction():
+    import torch
+    from ptmi import device
+    sa, cam, _ = scene_inputs('wavefront_comparison', 400)
+    ds = device.DeviceScene.from_arrays(sa, 'cuda')
+    assert ds.device.index == torch.cuda.current_device()
+    integ = device.Integrator(ds)
+    fr, acc = _frame_acc(cam, (100, 60, 64, 48))
+    integ.render_mk(fr, acc, 0, 2)
+    torch.cuda.synchronize()
+    ref = acc.cpu().numpy()
+    if torch.cuda.device_count() < 2:
+        # one GPU: a foreign-device stream must be refused, not used
+        class _Fake:
+            device = torch.device('cuda', 1)
+            cuda_stream = 0
+        with pytest.raises(Exception, match='stream is on'):
+            integ.render_mk(fr, acc, 0, 1, stream=_Fake())
+        return
+    # scene on cuda:1 while cuda:0 is current: the launch must go to cuda:1
+    torch.cuda.set_device(0)
+    ds1 = device.DeviceScene.from_arrays(sa, 'cuda:1')
+    integ1 = device.Integrator(ds1)
+    acc1 = torch.zeros_like(acc, device='cuda:1')
+    integ1.render_mk(fr, acc1, 0, 2)
+    torch.cuda.synchronize('cuda:1')
+    assert np.array_equal(acc1.cpu().numpy(), ref)
+
+
+def test_mk_staged_item_ids_past_2_to_32_split_into_batches():
+    import torch
+    from edge_scenes import edge_scene
+    from ptmi import device
+    sa, cam, bg = edge_scene('empty')
+    W, H = cam['width'], cam['height']
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, W, H, (0, 0, 1, 1))  # one pixel = one 8x8 tile
+    n = (1 << 26) + 3  # 64 * n item ids > 2^32
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
+    integ.reset_counters()
+    integ.render_mk(fr, acc, 0, n)
+    torch.cuda.synchronize()
+    assert integ.read_counters()['paths'] == n
+    # every sample of the empty scene is bg; the resolve adds them in sample order
+    want = np.add.accumulate(np.full(n, np.float32(bg[0]), np.float32))[-1]
+    assert acc[0, 0, 0].item() == want
+    assert acc[0, 1:].abs().sum().item() == 0.0

@@ -70,3 +70,14 @@ def test_mesh_scene_compiles():
     n = geom['num_spheres'] + qg['num_quads'] + tg['num_triangles']
     assert b['num_bvh_nodes'] == 2 * n - 1
     assert sd.leaf_depths(b).max() <= 62
+
+
+def test_leaf_depths_refuses_non_preorder_bvh():
+    # the stack size comes from these depths and the kernels push without a
+    # bound check, so a BVH whose children precede their parent is refused
+    b = {'bvh_left_child': np.array([-1, -1, 0], np.int32), 'bvh_right_child': np.array([-1, -1, 1], np.int32)}
+    import pytest
+    with pytest.raises(ValueError, match='preorder'):
+        sd.leaf_depths(b)
+    ok = {'bvh_left_child': np.array([1, -1, -1], np.int32), 'bvh_right_child': np.array([2, -1, -1], np.int32)}
+    assert sd.leaf_depths(ok).tolist() == [0, 1, 1]
