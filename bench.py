@@ -210,7 +210,7 @@ def main():
 
     sa, cam, bg, data_note = load_workload(a.scene, a.width)
     W, H = cam['width'], cam['height']
-    integ = device.Integrator(device.DeviceScene(sd.pack_device(sa), dev))
+    integ = device.Integrator(device.DeviceScene(sa, dev))
     shard = Shard(rank, world, a.shard)
     frame = device.make_frame(cam, bg, a.max_depth, a.seed, W, H, band=shard.band())
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
@@ -222,8 +222,11 @@ def main():
 
     for k in range(a.warmup):
         render(frame, acc, sample_base(k), sps)
+    # warm the collective too: RCCL sets up a collective's channels on its
+    # first call, which must not land in the timed region
+    reduce_accum(acc, dst=0)
     torch.cuda.synchronize(dev)
-    integ.clear(frame, acc)
+    acc.zero_()  # all rows: the warm-up reduce left other ranks' bands on the root
     integ.reset_counters()
     torch.cuda.synchronize(dev)
     if world > 1:

@@ -107,6 +107,13 @@ typedef struct ptmi_frame {
 int ptmi_version(void);
 const char *ptmi_last_error(void);
 
+/* Byte stride of the library's BVH node array (the `nodes` layout above):
+ * 80 for one child record per internal node, 256 for two-level packets
+ * (record 0 = the node's children, records 1 and 2 = child 0's and child 1's
+ * children, zero-filled when that child is a leaf; 16 B padding). Internal
+ * refs are node index x this stride. */
+int ptmi_node_bytes(void);
+
 /* Checks a scene view's counts, alignment and structural limits on the host. */
 int ptmi_scene_check(const ptmi_scene_view *scene);
 

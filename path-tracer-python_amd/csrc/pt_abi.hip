@@ -160,6 +160,8 @@ extern "C" {
 
 int ptmi_version(void) { return PTMI_ABI_VERSION; }
 
+int ptmi_node_bytes(void) { return (int)kNodeBytes; }
+
 const char* ptmi_last_error(void) { return g_err.c_str(); }
 
 int ptmi_scene_check(const ptmi_scene_view* scene) {

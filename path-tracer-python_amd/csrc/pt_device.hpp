@@ -366,6 +366,18 @@ __device__ unsigned long long g_probe[16];
 #define PTMI_NODE_CENTRES 1
 #endif
 
+#ifndef PTMI_TRAV2
+// Two-level node packets (include/ptmi.h, PTMI_NODE_BYTES): a popped node's
+// packet also holds both children's child records, so the step that expands
+// a node expands its near child in the same round trip (see trav_step).
+#define PTMI_TRAV2 0
+#endif
+#if PTMI_TRAV2
+constexpr uint32_t kNodeBytes = 256;
+#else
+constexpr uint32_t kNodeBytes = 80;
+#endif
+
 #ifndef PTMI_NODES_SGPR
 #define PTMI_NODES_SGPR 1  // megakernel: node base pinned in SGPRs (A/B with leaf preload: +0.8 % C2/C4)
 #endif
@@ -408,6 +420,108 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
     tr.sp += SB * 8;
   }
 }
+
+#if PTMI_TRAV2
+// Slab entry/exit of both children of one 80-B child record and their
+// projected centre distances (kernels.py:600-621, 707-713), as packed pairs.
+struct PairHit {
+  float E0, X0, E1, X1, d0, d1;
+};
+typedef float pt_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ PairHit pair_hit(const pt_f4v A, const pt_f4v B, const pt_f4v C, const pt_f4v R,
+                                            const pt_f4v Cxy, pt_f2 ox, pt_f2 oy, pt_f2 oz, pt_f2 ix, pt_f2 iy,
+                                            pt_f2 iz, pt_f2 dx, pt_f2 dy, pt_f2 dz, float tmin) {
+  const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
+  const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
+  const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
+  const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
+  const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
+  PairHit h;
+  h.E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
+  h.X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
+  h.E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
+  h.X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
+  const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
+  const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
+  h.d0 = dist.x;
+  h.d1 = dist.y;
+  return h;
+}
+
+// Expansion of a popped internal node P from its 256-B packet: record 0 holds
+// P's children (c0, c1), records 1 and 2 hold c0's and c1's children. The
+// reference (kernels.py:698-740) pushes P's far child, then its near child,
+// and pops the near child at once: with the same closest_t it tests the near
+// box against [t_min, closest_t] and, if internal and hit, pushes the near
+// child's far and near children. This step does exactly that in one round
+// trip: it pushes P's far child and then the near child's two children (or
+// the near child itself when it is a leaf). The stack holds the reference's
+// entries in the reference's order minus the near child's own entry, so
+// pops, culls and ties are unchanged, and the stack is never deeper than the
+// reference's (an expanded near child at depth d + 1 has children at depth
+// d + 2 <= max_leaf_depth: its three writes end at slot <= max_leaf_depth).
+template <int STACK, int SB>
+__device__ __forceinline__ void trav_expand2(const __attribute__((address_space(1))) pt_f4v* nodes, Trav& tr,
+                                             pt_v3 o, pt_v3 d, int32_t ref) {
+  typedef const __attribute__((address_space(1))) pt_f4v gf4;
+  constexpr uint32_t kSlot = SB * 8;
+  gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);
+#if PTMI_TRAV2 == 2
+  // record 0 only; the near child's record is loaded once the near child is
+  // known (a second, cache-hot round trip from the same packet, instead of
+  // holding both children's records in registers)
+  pt_f4v P[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) P[k] = nd[k];
+#else
+  pt_f4v P[15];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) P[k] = nd[k];
+#endif
+  const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
+  const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
+  const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
+  const float tmin = tr.tmin;
+  const PairHit h = pair_hit(P[0], P[1], P[2], P[3], P[4], ox, oy, oz, ix, iy, iz, dx, dy, dz, tmin);
+  const bool ln = h.d0 < h.d1;  // child 0 is the near one
+  const int32_t ref0 = __float_as_int(P[3].x), ref1 = __float_as_int(P[3].y);
+  const int32_t nref = ln ? ref0 : ref1, fref = ln ? ref1 : ref0;
+  const float nE = ln ? h.E0 : h.E1, fE = ln ? h.E1 : h.E0;
+  const bool nh = ln ? (h.X0 >= h.E0) : (h.X1 >= h.E1), fh = ln ? (h.X1 >= h.E1) : (h.X0 >= h.E0);
+  // the near child's pop, right after P's expansion: box hit and E <= closest_t
+  const bool coll = nh && nref >= 0 && nE <= tr.closest;
+  pt_f4v NA, NB, NC, NR, NCxy;
+#if PTMI_TRAV2 == 2
+  {
+    gf4* nn = nd + (ln ? 5 : 10);
+    NA = nn[0]; NB = nn[1]; NC = nn[2]; NR = nn[3]; NCxy = nn[4];
+  }
+#else
+  NA = ln ? P[5] : P[10];
+  NB = ln ? P[6] : P[11];
+  NC = ln ? P[7] : P[12];
+  NR = ln ? P[8] : P[13];
+  NCxy = ln ? P[9] : P[14];
+#endif
+  const PairHit g = pair_hit(NA, NB, NC, NR, NCxy, ox, oy, oz, ix, iy, iz, dx, dy, dz, tmin);
+  const bool gl = g.d0 < g.d1;
+  const int32_t g0 = __float_as_int(NR.x), g1 = __float_as_int(NR.y);
+  // entries above P's far child: the near child's far and near children, or the near child itself
+  const int32_t r2 = coll ? (gl ? g1 : g0) : nref;
+  const float e2 = coll ? (gl ? g.E1 : g.E0) : nE;
+  const bool b2 = coll ? (gl ? (g.X1 >= g.E1) : (g.X0 >= g.E0)) : nh;
+  const int32_t r3 = gl ? g0 : g1;
+  const float e3 = gl ? g.E0 : g.E1;
+  const bool b3 = coll && (gl ? (g.X0 >= g.E0) : (g.X1 >= g.E1));
+  const uint32_t s1 = tr.sp;
+  const uint32_t s2 = s1 + (fh ? kSlot : 0u);
+  const uint32_t s3 = s2 + (b2 ? kSlot : 0u);
+  lds_store2(s1, (uint32_t)fref, __float_as_uint(fE));
+  lds_store2(s2, (uint32_t)r2, __float_as_uint(e2));
+  if (coll) lds_store2(s3, (uint32_t)r3, __float_as_uint(e3));
+  tr.sp = s3 + (b3 ? kSlot : 0u);
+}
+#endif
 
 // One step of the traversal loop (one pop); precondition tr.busy().
 // A/B on MI355X (parity-identical): deferring a popped leaf's test to the next
@@ -514,6 +628,10 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
       atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
     }
   }
+#endif
+#if PTMI_TRAV2
+  trav_expand2<STACK, SB>(nodes, tr, o, d, ref);
+  return;
 #endif
   // internal: kernels.py:698-740, both children at once
   const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);

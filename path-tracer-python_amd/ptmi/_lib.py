@@ -48,7 +48,7 @@ class Frame(C.Structure):
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',
            'ptmi_mk_render_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
-           'ptmi_prof_stop')
+           'ptmi_prof_stop', 'ptmi_node_bytes')
 PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve', 'mk_resolve')
 
 _lib = None
@@ -80,6 +80,7 @@ def load(path: str = LIB_PATH):
     lib = C.CDLL(path)
     P = C.c_void_p
     lib.ptmi_version.restype = C.c_int
+    lib.ptmi_node_bytes.restype = C.c_int
     lib.ptmi_last_error.restype = C.c_char_p
     lib.ptmi_scene_check.argtypes = [C.POINTER(SceneView)]
     lib.ptmi_mk_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_int32, C.c_int32, P, P]

@@ -9,6 +9,7 @@ object, so several scenes can coexist in one process.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -36,7 +37,13 @@ class DeviceScene:
 
     def __init__(self, scene, device=None):
         require_gpu()
-        layout = scene if isinstance(scene, DeviceLayout) else pack_device(scene)
+        node_bytes = int(_lib.load().ptmi_node_bytes())
+        # PTMI_PACK_LEAF_ORDER=0: compile-order primitives (A/B timing only; same results)
+        leaf_order = os.environ.get('PTMI_PACK_LEAF_ORDER', '1') != '0'
+        layout = scene if isinstance(scene, DeviceLayout) else pack_device(scene, node_bytes, leaf_order)
+        if layout.n_inner and layout.nodes.shape[1] * 4 != node_bytes:
+            raise _lib.PtmiError(f'scene packed with {layout.nodes.shape[1] * 4}-B nodes, '
+                                 f'libptmi expects {node_bytes}')
         self.layout = layout
         dev = torch.device(device if device is not None else 'cuda')
         if dev.type != 'cuda':
@@ -86,7 +93,7 @@ class DeviceScene:
 
     @classmethod
     def from_arrays(cls, sa: SceneArrays, device=None):
-        return cls(pack_device(sa), device)
+        return cls(sa, device)
 
 
 def make_frame(cam, bg, max_depth, seed, width, height, window=None, band=(1, 1, 0)):

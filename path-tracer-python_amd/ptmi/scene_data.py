@@ -175,6 +175,7 @@ LEAF_FLAG = np.int64(0x80000000)
 
 NODE_FLOATS = 20  # 80-B internal node (include/ptmi.h)
 NODE_BYTES = 4 * NODE_FLOATS  # an internal child ref is the child's byte offset in the node array
+PACKET_BYTES = 256  # two-level node packet: 3 child records + 16 B padding
 
 
 def leaf_code(prim_type, prim_idx):
@@ -185,7 +186,7 @@ def leaf_code(prim_type, prim_idx):
 @dataclass
 class DeviceLayout:
     """Host-side arrays in the device layout of include/ptmi.h."""
-    nodes: np.ndarray       # (n_inner, NODE_FLOATS) f32
+    nodes: np.ndarray       # (n_inner, node_bytes / 4) f32
     root_ref: int
     root_min: np.ndarray
     root_max: np.ndarray
@@ -203,6 +204,9 @@ class DeviceLayout:
     num_spheres: int
     num_quads: int
     num_triangles: int
+    # device primitive k of type t is the reference's primitive prim_perm[t][k]
+    # (types indexed sphere 0, triangle 1, quad 2; identity unless leaf_order)
+    prim_perm: tuple = ()
 
     @property
     def n_inner(self):
@@ -260,7 +264,36 @@ def leaf_depths(bvh):
     return depth
 
 
-def pack_device(sa: SceneArrays) -> DeviceLayout:
+def leaf_order_perm(bvh, counts):
+    """Per primitive type, the reference's primitive indices in the order the
+    preorder flattened BVH reaches their leaves (index order is preorder,
+    sah_bvh_builder.py:338-418). Laying the device primitives and materials
+    out in this order puts primitives that share a subtree, and are therefore
+    tested by the same rays one after the other, on the same cache lines; the
+    reference's compile order (scene_compiler.py:931) follows scene
+    construction, which for vol2's 1000 randomly placed spheres is spatially
+    random."""
+    ptype, pidx = bvh['bvh_prim_type'], bvh['bvh_prim_idx']
+    leaves = np.nonzero(pidx >= 0)[0]
+    perm = []
+    for t, n in enumerate(counts):
+        order = pidx[leaves[ptype[leaves] == t]].astype(np.int64)
+        if order.shape[0] != n or (n and not np.array_equal(np.sort(order), np.arange(n))):
+            raise ValueError(f'BVH leaves of type {t} are not a permutation of the {n} primitives')
+        perm.append(order)
+    return tuple(perm)
+
+
+def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True) -> DeviceLayout:
+    """Reference-layout arrays -> include/ptmi.h device layout. ``node_bytes``
+    is the library's node stride (ptmi_node_bytes()): 80 for one child record
+    per internal node, 256 for two-level packets (record 0: the node's
+    children; records 1 and 2: each child's children, zero for a leaf
+    child). ``leaf_order`` renumbers each primitive type in BVH leaf order
+    (leaf_order_perm); leaf codes, primitive and material rows are permuted
+    together, so every lookup the kernels make finds the same data and the
+    traversal visits the same leaves in the same order: results are
+    unchanged bit for bit."""
     ns, nq, nt = sa.num_spheres, sa.num_quads, sa.num_triangles
     b = sa.bvh
     bmin, bmax = b['bvh_bbox_min'], b['bvh_bbox_max']
@@ -275,10 +308,23 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
         raise ValueError('internal BVH node with a missing child')
     cidx = np.full(n, -1, np.int64)
     cidx[internal] = np.arange(internal.shape[0])
-    codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | pidx.astype(np.int64)) - (1 << 32)).astype(np.int32)
-    if internal.shape[0] * NODE_BYTES > 0x7fffffff:
+    counts = (ns, nt, nq)  # by prim type code: sphere 0, triangle 1, quad 2
+    if leaf_order and n:
+        perm = leaf_order_perm(b, counts)
+    else:
+        perm = tuple(np.arange(c, dtype=np.int64) for c in counts)
+    new_idx = pidx.astype(np.int64).copy()
+    for t in range(3):
+        inv = np.empty(counts[t], np.int64)
+        inv[perm[t]] = np.arange(counts[t])
+        sel = is_leaf & (ptype == t)
+        new_idx[sel] = inv[pidx[sel]]
+    codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | new_idx) - (1 << 32)).astype(np.int32)
+    if node_bytes not in (NODE_BYTES, PACKET_BYTES):
+        raise ValueError(f'unsupported node stride {node_bytes}')
+    if internal.shape[0] * node_bytes > 0x7fffffff:
         raise ValueError(f'{internal.shape[0]} internal BVH nodes: byte offsets exceed int32')
-    refs = np.where(is_leaf, codes, (cidx * NODE_BYTES).astype(np.int32)).astype(np.int32)
+    refs = np.where(is_leaf, codes, (cidx * node_bytes).astype(np.int32)).astype(np.int32)
     nodes = np.zeros((internal.shape[0], NODE_FLOATS), np.float32)
     if internal.size:  # children interleaved per component (include/ptmi.h)
         l, r = left[internal], right[internal]
@@ -293,13 +339,22 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
         nodes[:, 14], nodes[:, 15] = cl[:, 2], cr[:, 2]
         nodes[:, 16], nodes[:, 17] = cl[:, 0], cr[:, 0]
         nodes[:, 18], nodes[:, 19] = cl[:, 1], cr[:, 1]
+    if node_bytes == PACKET_BYTES:  # two-level packets: the node's record, then each internal child's
+        pk = np.zeros((internal.shape[0], PACKET_BYTES // 4), np.float32)
+        pk[:, :NODE_FLOATS] = nodes
+        if internal.size:
+            for k, ch in ((1, left[internal]), (2, right[internal])):
+                inner = cidx[ch] >= 0
+                pk[inner, k * NODE_FLOATS:(k + 1) * NODE_FLOATS] = nodes[cidx[ch[inner]]]
+        nodes = pk
     if n:
         root_ref = int(refs[0])
         root_min, root_max = bmin[0].copy(), bmax[0].copy()
         max_leaf_depth = int(leaf_depths(b).max())
     else:
         root_ref, root_min, root_max, max_leaf_depth = 0, np.zeros(3, np.float32), np.zeros(3, np.float32), 0
-    spheres = np.ascontiguousarray(sa.sphere_data, np.float32).reshape(ns, 4)
+    ps, pt, pq = perm
+    spheres = np.ascontiguousarray(np.asarray(sa.sphere_data, np.float32).reshape(ns, 4)[ps])
     q = sa.quads
     quads = np.zeros((nq, 16), np.float32)
     quads[:, 0:3] = q['quad_normal']
@@ -314,8 +369,9 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
     tris[:, 3:6] = t['triangle_edge1']
     tris[:, 6:9] = t['triangle_edge2']
     tris[:, 9:12] = t['triangle_normal']
-    mats = np.concatenate([_pack_mats(sa.sphere_mats, ns), _pack_mats(sa.quad_mats, nq),
-                           _pack_mats(sa.tri_mats, nt)], axis=0)
+    quads, tris = quads[pq], tris[pt]
+    mats = np.concatenate([_pack_mats(sa.sphere_mats, ns)[ps], _pack_mats(sa.quad_mats, nq)[pq],
+                           _pack_mats(sa.tri_mats, nt)[pt]], axis=0)
     if len(sa.images) > MAX_IMAGES:
         raise ValueError(f'at most {MAX_IMAGES} image textures')
     texels, offs, ws, hs, off = [], [], [], [], 0
@@ -331,12 +387,12 @@ def pack_device(sa: SceneArrays) -> DeviceLayout:
     texels = np.concatenate(texels) if texels else np.zeros(1, np.uint32)
     pv = np.zeros((256, 4), np.float32)
     pv[:, :3] = sa.perlin['perlin_randvec']
-    perm = np.concatenate([sa.perlin['perlin_perm_x'], sa.perlin['perlin_perm_y'],
-                           sa.perlin['perlin_perm_z']]).astype(np.int32)
-    if perm.min() < 0 or perm.max() > 255:
+    pperm = np.concatenate([sa.perlin['perlin_perm_x'], sa.perlin['perlin_perm_y'],
+                            sa.perlin['perlin_perm_z']]).astype(np.int32)
+    if pperm.min() < 0 or pperm.max() > 255:
         raise ValueError('Perlin permutation out of range')
     return DeviceLayout(nodes, root_ref, root_min, root_max, max_leaf_depth, spheres, quads, tris, mats,
-                        texels, offs, ws, hs, pv, perm, ns, nq, nt)
+                        texels, offs, ws, hs, pv, pperm, ns, nq, nt, perm)
 
 
 def compile_world(world, perlin_tables=None):
