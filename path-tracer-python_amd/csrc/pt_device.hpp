@@ -138,6 +138,29 @@ __device__ __forceinline__ void get_ray(const DevFrame& fr, int32_t px, int32_t 
 #ifndef PTMI_LEAF_PRELOAD
 #define PTMI_LEAF_PRELOAD 1  // A/B on MI355X: +1.4 % C2, +4 % C4, +2.6 % wavefront
 #endif
+#ifndef PTMI_MASK_PRED
+#define PTMI_MASK_PRED 1
+#endif
+// a && b && c && d of per-lane compares as lane masks (v_cmp into SGPR pairs,
+// s_and): the compiler otherwise materialises each compare with v_cndmask and
+// combines them with 16-bit VALU bit ops (~16 VALU per quad test on gfx950)
+__device__ __forceinline__ bool pt_all4(bool a, bool b, bool c, bool d) {
+#if PTMI_MASK_PRED
+  return __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b) &
+                                             __builtin_amdgcn_ballot_w64(c) & __builtin_amdgcn_ballot_w64(d));
+#else
+  return a && b && c && d;
+#endif
+}
+
+__device__ __forceinline__ bool pt_all2(bool a, bool b) {
+#if PTMI_MASK_PRED
+  return __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b));
+#else
+  return a && b;
+#endif
+}
+
 // Each returns the candidate t (hit only if returned true); hit point and
 // normal are recomputed at shading time from (o, d, t) with the same
 // operation order the reference uses inside the hit functions.
@@ -163,7 +186,7 @@ __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, f
     float sq = sqrtf(disc);
     float root = (h - sq) / a;
     if (root < tmin || root > tmax) root = (h + sq) / a;
-    if (root >= tmin && root <= tmax) { t = root; return true; }
+    if (pt_all2(root >= tmin, root <= tmax)) { t = root; return true; }
   }
   return false;
 }
@@ -187,14 +210,14 @@ __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const
 #endif
   if (fabsf(denom) >= 1e-8f) {
     float tt = (a.w - pt_dot(n, o)) / denom;
-    if (tt >= tmin && tt <= tmax) {
+    if (pt_all2(tt >= tmin, tt <= tmax)) {
       pt_v3 Q = pt_v3f(b.x, b.y, b.z), u = pt_v3f(b.w, c.x, c.y), v = pt_v3f(c.z, c.w, e.x);
       pt_v3 w = pt_v3f(e.y, e.z, e.w);
       pt_v3 ip = pt_add(o, pt_scale(d, tt));
       pt_v3 pv = pt_sub(ip, Q);
       float alpha = pt_dot(w, pt_cross(pv, v));
       float beta = pt_dot(w, pt_cross(u, pv));
-      if (alpha >= 0.0f && alpha <= 1.0f && beta >= 0.0f && beta <= 1.0f) { t = tt; return true; }
+      if (pt_all4(alpha >= 0.0f, alpha <= 1.0f, beta >= 0.0f, beta <= 1.0f)) { t = tt; return true; }
     }
   }
   return false;
@@ -237,12 +260,12 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
     float inv = 1.0f / det;
     pt_v3 s = pt_sub(o, v0);
     float u = inv * pt_dot(s, hv);
-    if (u >= 0.0f && u <= 1.0f) {
+    if (pt_all2(u >= 0.0f, u <= 1.0f)) {
       pt_v3 q = pt_cross(s, e1);
       float v = inv * pt_dot(d, q);
-      if (v >= 0.0f && u + v <= 1.0f) {
+      if (pt_all2(v >= 0.0f, u + v <= 1.0f)) {
         float tt = inv * pt_dot(e2, q);
-        if (tt >= tmin && tt <= tmax) { t = tt; return true; }
+        if (pt_all2(tt >= tmin, tt <= tmax)) { t = tt; return true; }
       }
     }
   }
