@@ -709,12 +709,19 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
 }
 
+#ifndef PTMI_TRAV_UNROLL
+#define PTMI_TRAV_UNROLL 3  // pops per loop test in traverse() (wavefront kernels; A/B: 3 +0.5 % C3 / mesh fog, 2 +0.3 %)
+#endif
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
                                          float& t_out, int32_t& ref_out) {
   Trav tr;
   trav_begin<STACK, SB>(sc, tr, st, d, o, tmin, tmax);
-  while (tr.busy()) trav_step<STACK, SB>(sc, sc.nodes, tr, st, o, d);
+  while (tr.busy()) {
+#pragma unroll
+    for (int u = 0; u < PTMI_TRAV_UNROLL; ++u)
+      if (u == 0 || tr.busy()) trav_step<STACK, SB>(sc, sc.nodes, tr, st, o, d);
+  }
   t_out = tr.closest;
   ref_out = tr.best;
   return tr.any();
