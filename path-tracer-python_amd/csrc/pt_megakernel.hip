@@ -81,6 +81,9 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_HOLD_NOISE
 #define PTMI_MK_HOLD_NOISE 0  // A/B: 4 or 8 held lanes -1 to -1.5 % (profiles/r01/ab_mk_hold_noise.log)
 #endif
+#ifndef PTMI_MK_NT
+#define PTMI_MK_NT 0
+#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -390,9 +393,16 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
           const size_t srel = (size_t)(l.s - s_begin);
           float* o = staging + 3 * (srel * npix + (size_t)(l.row + (ip >> 3)) * (size_t)fr.w +
                                     (size_t)(l.x + (ip & 7) - fr.x0));
+#if PTMI_MK_NT
+          // A/B knob: non-temporal staging stores, +-0.3 % (profiles/r02/ab/ab_nontemporal.log)
+          __builtin_nontemporal_store(ps.color.x, o);
+          __builtin_nontemporal_store(ps.color.y, o + 1);
+          __builtin_nontemporal_store(ps.color.z, o + 2);
+#else
           o[0] = ps.color.x;
           o[1] = ps.color.y;
           o[2] = ps.color.z;
+#endif
           live = false;
         } else {  // render_sample: accum += color (kernels.py:1187), next sample of the same pixel
           acc = pt_add(acc, ps.color);

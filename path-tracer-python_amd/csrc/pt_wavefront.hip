@@ -163,22 +163,71 @@ struct Ray {
   uint32_t item, ctr, meta;
 };
 
+// Streamed buffers (queue records, hit records, medium lists, staging) go
+// through these helpers, with a cache-policy knob PTMI_WF_NT: 1 `nt` loads
+// and stores, 2 `nt` stores, 3 `sc1` stores (written line dropped from L2).
+// PMC: wf_intersect's L2 hit rate is 60 % against the megakernel's 96 %
+// (L1 hit rates 96 % / 98 %), the queue stream evicting BVH lines. But the
+// stage kernels re-read what the previous one wrote, and that reuse is worth
+// more: A/B on MI355X (parity-identical) C3 -10 % / -5 % / -5 %
+// (profiles/r02/ab/ab_nontemporal.log, profiles/r02/pmc_cache/).
+#ifndef PTMI_WF_NT
+#define PTMI_WF_NT 0
+#endif
+typedef float pt_qf4 __attribute__((ext_vector_type(4)));
+typedef float pt_qf2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T s_load(const T* p) {
+#if PTMI_WF_NT == 1
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void s_store(T* p, T v) {
+#if PTMI_WF_NT == 3
+  // s_nop: the store reads its data VGPRs after issue (VMEM store data
+  // hazard), which the compiler cannot see through inline asm
+  if constexpr (sizeof(T) == 16)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  else if constexpr (sizeof(T) == 8)
+    asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  else
+    asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+#elif PTMI_WF_NT == 1 || PTMI_WF_NT == 2
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ float4 q_load(const float4* p) {
+  const pt_qf4 v = s_load((const pt_qf4*)p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void q_store(float4* p, float4 v) { s_store((pt_qf4*)p, pt_qf4{v.x, v.y, v.z, v.w}); }
+__device__ __forceinline__ float2 h_load(const float2* p) {
+  const pt_qf2 v = s_load((const pt_qf2*)p);
+  return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ void h_store(float2* p, float2 v) { s_store((pt_qf2*)p, pt_qf2{v.x, v.y}); }
+
 __device__ __forceinline__ void store_ray(const Queue& q, int32_t i, const Ray& r) {
-  q.a[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-  q.b[i] = make_float4(r.d.y, r.d.z, r.thr.x, r.thr.y);
-  q.c[i] = make_float4(r.thr.z, __uint_as_float(r.item), __uint_as_float(r.ctr), __uint_as_float(r.meta));
+  q_store(q.a + i, make_float4(r.o.x, r.o.y, r.o.z, r.d.x));
+  q_store(q.b + i, make_float4(r.d.y, r.d.z, r.thr.x, r.thr.y));
+  q_store(q.c + i, make_float4(r.thr.z, __uint_as_float(r.item), __uint_as_float(r.ctr), __uint_as_float(r.meta)));
 }
 
 __device__ __forceinline__ void kill_slot(const Queue& q, int32_t i) {
-  reinterpret_cast<uint32_t*>(q.c + i)[1] = kDead;
+  s_store(reinterpret_cast<uint32_t*>(q.c + i) + 1, kDead);
 }
 
 __device__ __forceinline__ uint32_t slot_item(const Queue& q, int32_t i) {
-  return reinterpret_cast<const uint32_t*>(q.c + i)[1];
+  return s_load(reinterpret_cast<const uint32_t*>(q.c + i) + 1);
 }
 
 __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
-  float4 a = q.a[i], b = q.b[i], c = q.c[i];
+  float4 a = q_load(q.a + i), b = q_load(q.b + i), c = q_load(q.c + i);
   Ray r;
   r.o = pt_v3f(a.x, a.y, a.z);
   r.d = pt_v3f(a.w, b.x, b.y);
@@ -235,9 +284,9 @@ __device__ __forceinline__ Ray camera_ray(const DevFrame& fr, const WfBufs& wb, 
 __device__ __forceinline__ void stage(const DevFrame& fr, const WfBufs& wb, uint32_t k, pt_v3 c) {
   const Item it = decode_item(fr, wb, k);
   float* p = wb.staging + 3 * ((size_t)it.srel * (size_t)wb.npix + (size_t)it.p);
-  p[0] = c.x;
-  p[1] = c.y;
-  p[2] = c.z;
+  s_store(p, c.x);
+  s_store(p + 1, c.y);
+  s_store(p + 2, c.z);
 }
 
 __device__ __forceinline__ int32_t shard_end(const WfBufs& wb, int32_t s) {
@@ -341,12 +390,12 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
     assign_work(fr, wb, i, item);  // generate_camera_rays (kernels.py:1219-1239) for slots that need work
     if (item >= kPending) continue;
     ++n_live;
-    float4 a = q.a[i], b = q.b[i];
+    float4 a = q_load(q.a + i), b = q_load(q.b + i);
     pt_v3 o = pt_v3f(a.x, a.y, a.z), d = pt_v3f(a.w, b.x, b.y);
     float t;
     int32_t ref;
     bool hit = traverse<STACK, kWfBlock>(sc, o, d, kTMin, kTMax, st, t, ref);
-    wb.hit[i] = make_float2(t, __int_as_float(hit ? ref : kMissRef));
+    h_store(wb.hit + i, make_float2(t, __int_as_float(hit ? ref : kMissRef)));
   }
   if (counters) block_flush(n_live, lds_stack, counters + 0);
 }
@@ -380,7 +429,7 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
 // wf_intersect hands it the next item of its group's chunk).
 __device__ __forceinline__ void finish_lane(const WfBufs& wb, int32_t i, bool ended, bool go, const Ray& cont) {
   if (go) store_ray(wb.q, i, cont);
-  if (ended) reinterpret_cast<uint32_t*>(wb.q.c + i)[1] = kPending;
+  if (ended) s_store(reinterpret_cast<uint32_t*>(wb.q.c + i) + 1, kPending);
 }
 
 // Surface branch of shade_and_scatter (kernels.py:1359-1399) for slot ray
@@ -429,7 +478,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
     Ray cont;
     const bool live = i < wb.capacity && slot_item(q, i) < kPending;
     if (live) {
-      const float2 h = wb.hit[i];
+      const float2 h = h_load(wb.hit + i);
       const int32_t ref = __float_as_int(h.y);
       const Ray ray = load_ray(q, i);
       if (ref == kMissRef) {
@@ -448,12 +497,12 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
       }
     }
     const int32_t mslot = wave_ticket(to_medium, ctl_medium(wb, shard));
-    if (to_medium) wb.medq[shard * wb.medseg + mslot] = i;
+    if (to_medium) s_store(wb.medq + shard * wb.medseg + mslot, i);
 #if PTMI_WF_DEFER_NOISE
     // deferred hits fill the shard's segment from the top; a slot is in at
     // most one of the two lists, so together they never exceed the segment
     const int32_t nslot = wave_ticket(to_noise, ctl_noise(wb, shard));
-    if (to_noise) wb.medq[shard * wb.medseg + wb.medseg - 1 - nslot] = i;
+    if (to_noise) s_store(wb.medq + shard * wb.medseg + wb.medseg - 1 - nslot, i);
 #endif
     finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
@@ -506,8 +555,8 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
           shard = s + 1;
         }
       }
-      i = wb.medq[shard * wb.medseg + wb.medseg - 1 - off];
-      const float2 h = wb.hit[i];
+      i = s_load(wb.medq + shard * wb.medseg + wb.medseg - 1 - off);
+      const float2 h = h_load(wb.hit + i);
       const int32_t ref = __float_as_int(h.y);
       shade_surface(sc, fr, wb, load_ray(wb.q, i), h.x, ref, mat_index(sc, ref), ended, go, cont);
     }
@@ -521,8 +570,8 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
           shard = s + 1;
         }
       }
-      i = wb.medq[shard * wb.medseg + off];
-      const float2 h = wb.hit[i];
+      i = s_load(wb.medq + shard * wb.medseg + off);
+      const float2 h = h_load(wb.hit + i);
       const int32_t ref = __float_as_int(h.y);
       const Ray ray = load_ray(wb.q, i);
       const float t_entry = h.x;
