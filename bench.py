@@ -92,6 +92,9 @@ def parse():
     p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
                    help='nccl = RCCL over xGMI (the product path); gloo only to rehearse the multi-rank flow '
                         'with several ranks on one GPU (host-side reduce)')
+    p.add_argument('--traversal', choices=('stack', 'stackless'), default='stack',
+                   help="BVH traversal: the reference's default stack walk (traverse_bvh_legacy, kernels.py:625) "
+                        'or its USE_STACKLESS_TRAVERSAL walk (traverse_bvh_stackless, kernels.py:453)')
     p.add_argument('--shard', choices=('samples', 'tiles'), default='samples',
                    help='multi-GPU partition: disjoint sample shards (weak scaling) or row-band tiles (strong)')
     a = p.parse_args()
@@ -212,7 +215,7 @@ def main():
     W, H = cam['width'], cam['height']
     integ = device.Integrator(device.DeviceScene(sa, dev))
     shard = Shard(rank, world, a.shard)
-    frame = device.make_frame(cam, bg, a.max_depth, a.seed, W, H, band=shard.band())
+    frame = device.make_frame(cam, bg, a.max_depth, a.seed, W, H, band=shard.band(), traversal=a.traversal)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     render = integ.render_mk if a.variant == 'mk' else integ.render_wf
     sps = a.spp_per_step
@@ -298,7 +301,8 @@ def main():
         'config': {
             'workload': f'{a.scene} {W}x{H}, {"wavefront" if a.variant == "wf" else "megakernel"} integrator, '
                         f'{sps * a.steps} spp per GPU ({a.steps} steps x {sps} spp), max_depth {a.max_depth}',
-            'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'spp_per_step': sps,
+            'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'traversal': a.traversal,
+            'spp_per_step': sps,
             'spp_per_gpu': sps * a.steps if a.shard == 'samples' else f'{sps * a.steps} (rows 1/{world})', 'max_depth': a.max_depth, 'seed': a.seed,
             'parallelism': (f'{a.shard}-shard x{world} + {"RCCL" if a.dist_backend == "nccl" else "gloo"} reduce'
                             if world > 1 else 'single GPU'),

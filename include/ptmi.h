@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 4
+#define PTMI_ABI_VERSION 5
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -59,6 +59,13 @@ enum {
  *   texels  : RGBA8 texels of all image textures, image k at img_offset[k]
  *   perlin_vec  : 256 x 4 f32 (randvec, w unused)
  *   perlin_perm : 3 x 256 i32 (perm_x, perm_y, perm_z)
+ *   ref_nodes   : num_bvh_nodes x 12 f32 (48 B), the reference's own
+ *             flattened nodes in its preorder (sah_bvh_builder.py:338-418,
+ *             fields.py:52-63) for the stackless traversal
+ *             (PTMI_TRAV_STACKLESS): {min.xyz, left | max.xyz, right |
+ *             parent, leaf code (0 = internal), side, 0} (i32 bits), side = 0
+ *             when the node is its parent's left child, else 1. May be NULL
+ *             when no frame asks for the stackless traversal.
  */
 typedef struct ptmi_scene_view {
     const float *nodes;
@@ -76,6 +83,8 @@ typedef struct ptmi_scene_view {
     int32_t img_offset[PTMI_MAX_IMAGES], img_w[PTMI_MAX_IMAGES], img_h[PTMI_MAX_IMAGES];
     const float *perlin_vec;
     const int32_t *perlin_perm;
+    const float *ref_nodes;
+    int32_t num_bvh_nodes;     /* all nodes: 2 x primitives - 1 (0 for an empty world) */
 } ptmi_scene_view;
 
 /* Camera upload values (renderer.py:230-247 / fields.py:159-165). */
@@ -83,6 +92,13 @@ typedef struct ptmi_camera {
     float center[3], pixel00[3], delta_u[3], delta_v[3], defocus_u[3], defocus_v[3];
     float defocus_angle;
 } ptmi_camera;
+
+/* BVH traversal (traverse_bvh, kernels.py:749-759, switched by the module
+ * constant USE_STACKLESS_TRAVERSAL, kernels.py:746): the reference's default
+ * stack traversal with front-to-back child order (traverse_bvh_legacy,
+ * kernels.py:625-742), or its parent-pointer stackless traversal, left child
+ * first (traverse_bvh_stackless, kernels.py:453-597; needs ref_nodes). */
+enum { PTMI_TRAV_STACK = 0, PTMI_TRAV_STACKLESS = 1 };
 
 /* One render request: camera + render state (fields.py:171-172) + the pixel
  * set this call owns. The pixel set is the window [x0,x0+w) x [y0,y0+h)
@@ -97,6 +113,7 @@ typedef struct ptmi_frame {
     int32_t width, height;
     int32_t x0, y0, w, h;
     int32_t band_rows, band_stride, band_offset;
+    int32_t traversal;         /* PTMI_TRAV_* */
 } ptmi_frame;
 
 /* Device counters (u64): [0] ray segments traced from the depth loop / waves,

@@ -34,13 +34,13 @@ class OrScene(C.Structure):
                 ('bvh_min', P), ('bvh_max', P), ('bvh_left', P), ('bvh_right', P), ('bvh_type', P), ('bvh_idx', P),
                 ('perlin_vec', P), ('perm_x', P), ('perm_y', P), ('perm_z', P),
                 ('num_images', C.c_int32), ('images', P * MAX_IMAGES), ('img_w', C.c_int32 * MAX_IMAGES),
-                ('img_h', C.c_int32 * MAX_IMAGES)]
+                ('img_h', C.c_int32 * MAX_IMAGES), ('bvh_parent', P)]
 
 
 class OrFrame(C.Structure):
     _fields_ = [('center', f3), ('pixel00', f3), ('delta_u', f3), ('delta_v', f3), ('defocus_u', f3),
                 ('defocus_v', f3), ('defocus_angle', C.c_float), ('bg', f3), ('max_depth', C.c_int32),
-                ('seed', C.c_uint32), ('width', C.c_int32), ('height', C.c_int32)]
+                ('seed', C.c_uint32), ('width', C.c_int32), ('height', C.c_int32), ('traversal', C.c_int32)]
 
 
 class OrStats(C.Structure):
@@ -62,7 +62,7 @@ def load():
         lib = C.CDLL(LIB)
         lib.or_render.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, P, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OrStats)]
-        lib.or_traverse.argtypes = [C.POINTER(OrScene), P, P, C.c_float, C.c_float, P, P, P]
+        lib.or_traverse.argtypes = [C.POINTER(OrScene), C.c_int, P, P, C.c_float, C.c_float, P, P, P]
         lib.or_trace_path.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, C.c_int, C.c_int, C.c_int,
                                       P, C.POINTER(OrStats)]
         lib.or_math_probe.argtypes = [C.c_int, P, P, P, C.c_int]
@@ -117,6 +117,7 @@ class OracleScene:
         s.bvh_min, s.bvh_max = c(b['bvh_bbox_min'], f32), c(b['bvh_bbox_max'], f32)
         s.bvh_left, s.bvh_right = c(b['bvh_left_child'], i32), c(b['bvh_right_child'], i32)
         s.bvh_type, s.bvh_idx = c(b['bvh_prim_type'], i32), c(b['bvh_prim_idx'], i32)
+        s.bvh_parent = c(b['bvh_parent'], i32)
         p = sa.perlin
         s.perlin_vec = c(p['perlin_randvec'], f32)
         s.perm_x, s.perm_y, s.perm_z = c(p['perlin_perm_x'], i32), c(p['perlin_perm_y'], i32), c(p['perlin_perm_z'], i32)
@@ -128,8 +129,12 @@ class OracleScene:
         self._keep = keep
 
 
-def make_frame(cam, bg, max_depth, seed, width, height):
+TRAVERSALS = {'stack': 0, 'stackless': 1}  # traverse_bvh_legacy / traverse_bvh_stackless (kernels.py:746)
+
+
+def make_frame(cam, bg, max_depth, seed, width, height, traversal='stack'):
     f = OrFrame()
+    f.traversal = TRAVERSALS[traversal]
     for k in ('center', 'pixel00', 'delta_u', 'delta_v', 'defocus_u', 'defocus_v'):
         v = np.asarray(cam[k], np.float32)
         for i in range(3):
@@ -155,13 +160,13 @@ def render(oscene, frame, variant, accum, window, s_begin, s_count, threads=0):
     return {'segments': st.segments, 'medium': st.medium, 'paths': st.paths}
 
 
-def traverse(oscene, o, d, tmin=0.001, tmax=1e10):
+def traverse(oscene, o, d, tmin=0.001, tmax=1e10, traversal='stack'):
     o = np.asarray(o, np.float32)
     d = np.asarray(d, np.float32)
     t = np.zeros(1, np.float32)
     ty = np.zeros(1, np.int32)
     ix = np.zeros(1, np.int32)
-    hit = load().or_traverse(C.byref(oscene.s), _ptr(o), _ptr(d), tmin, tmax, _ptr(t), _ptr(ty), _ptr(ix))
+    hit = load().or_traverse(C.byref(oscene.s), TRAVERSALS[traversal], _ptr(o), _ptr(d), tmin, tmax, _ptr(t), _ptr(ty), _ptr(ix))
     return bool(hit), float(t[0]), int(ty[0]), int(ix[0])
 
 

@@ -296,11 +296,75 @@ static int traverse_bvh(const or_scene *sc, pt_v3 o, pt_v3 d, float tmin, float 
     return any;
 }
 
+static int traverse_bvh_stackless(const or_scene *sc, pt_v3 o, pt_v3 d, float tmin, float tmax, hit_t *out) {
+    /* traverse_bvh_stackless, kernels.py:453-597 (selected when
+       USE_STACKLESS_TRAVERSAL, :746): left child first, parent pointers,
+       at most 2 * num_bvh_nodes loop iterations (:487-491) */
+    hit_t best; memset(&best, 0, sizeof best);
+    float closest = tmax;
+    int any = 0;
+    pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f,   /* :478-482 */
+                       fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                       fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);
+    int32_t node = 0;
+    int came = -1;   /* -1 none, 0 left, 1 right (:484-485) */
+    int64_t max_it = (int64_t)sc->num_bvh_nodes * 2, it = 0;
+    while (node >= 0 && it < max_it) {
+        ++it;
+        int up = 0;   /* ascend to the parent this iteration */
+        if (came == 0) {                                      /* :497-510 */
+            int32_t r = sc->bvh_right[node];
+            if (r >= 0) { node = r; came = -1; continue; }
+            up = 1;
+        } else if (came == 1) {                               /* :511-520 */
+            up = 1;
+        } else if (!hit_aabb(sc->bvh_min + 3 * node, sc->bvh_max + 3 * node, o, inv, tmin, closest)) {
+            up = 1;                                           /* :523-533 */
+        } else if (sc->bvh_idx[node] >= 0) {                  /* leaf, :536-571 */
+            int32_t pidx = sc->bvh_idx[node], ptype = sc->bvh_type[node];
+            hit_t h; int hit = 0;
+            if (ptype == OR_SPHERE) hit = hit_sphere(sc, pidx, o, d, tmin, closest, &h);
+            else if (ptype == OR_TRIANGLE) hit = hit_triangle(sc, pidx, o, d, tmin, closest, &h);
+            else if (ptype == OR_QUAD) hit = hit_quad(sc, pidx, o, d, tmin, closest, &h);
+            if (hit && h.t < closest) {
+                any = 1;
+                closest = h.t;
+                best = h;
+                best.type = ptype;
+                best.idx = pidx;
+            }
+            up = 1;
+        } else {                                              /* internal, :572-595 */
+            int32_t l = sc->bvh_left[node], r = sc->bvh_right[node];
+            if (l >= 0) { node = l; came = -1; }
+            else if (r >= 0) { node = r; came = -1; }
+            else up = 1;
+        }
+        if (up) {   /* parent_idx >= 0: came = which child we were; else done */
+            int32_t p = sc->bvh_parent[node];
+            if (p < 0) break;
+            came = (sc->bvh_left[p] == node) ? 0 : 1;
+            node = p;
+        }
+    }
+    best.hit = any;
+    best.t = closest;
+    if (!any) { best.t = 0.0f; best.type = 0; best.idx = 0; }
+    *out = best;
+    return any;
+}
+
+static int traverse(const or_scene *sc, int mode, pt_v3 o, pt_v3 d, float tmin, float tmax, hit_t *out) {
+    /* traverse_bvh, kernels.py:749-759 */
+    return mode == OR_TRAV_STACKLESS ? traverse_bvh_stackless(sc, o, d, tmin, tmax, out)
+                                     : traverse_bvh(sc, o, d, tmin, tmax, out);
+}
+
 /* ---------------- constant medium, kernels.py:365-450 ---------------- */
 
 typedef struct medium_t { int is_hit; float t_scatter; pt_v3 p; float t_exit; } medium_t;
 
-static medium_t apply_constant_medium(const or_scene *sc, int pt, int pi, pt_v3 o, pt_v3 d,
+static medium_t apply_constant_medium(const or_scene *sc, int mode, int pt, int pi, pt_v3 o, pt_v3 d,
                                       float tmin, float tmax, float t_entry, rng_t *r, or_stats *st) {
     medium_t m; m.is_hit = 0; m.t_scatter = 0.0f; m.p = pt_v3f(0.0f, 0.0f, 0.0f); m.t_exit = 0.0f;
     int is_med = sc->is_medium[pt][pi];
@@ -308,7 +372,7 @@ static medium_t apply_constant_medium(const or_scene *sc, int pt, int pi, pt_v3 
     if (is_med > 0) {
         hit_t ex;
         if (st) st->medium++;
-        int hit_exit = traverse_bvh(sc, o, d, t_entry + 0.0001f, 1e10f, &ex);
+        int hit_exit = traverse(sc, mode, o, d, t_entry + 0.0001f, 1e10f, &ex);
         if (hit_exit) {
             m.t_exit = ex.t;
             float t1 = pt_maxf(t_entry, tmin);
@@ -424,7 +488,7 @@ static pt_v3 trace_ray_mk(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
     for (int depth = 0; depth < fr->max_depth; ++depth) {
         hit_t h;
         if (st) st->segments++;
-        int hit = traverse_bvh(sc, o, d, 0.001f, 1e10f, &h);
+        int hit = traverse(sc, fr->traversal, o, d, 0.001f, 1e10f, &h);
         if (hit) {
             int pt = h.type, pi = h.idx;
             int is_med = sc->is_medium[pt][pi];
@@ -432,7 +496,7 @@ static pt_v3 trace_ray_mk(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
             pt_v3 sdir = pt_v3f(0.0f, 0.0f, 0.0f), att = pt_v3f(1.0f, 1.0f, 1.0f);
             pt_v3 hp = h.p, n = h.n;
             if (is_med > 0) {
-                medium_t m = apply_constant_medium(sc, pt, pi, o, d, 0.001f, 1e10f, h.t, r, st);
+                medium_t m = apply_constant_medium(sc, fr->traversal, pt, pi, o, d, 0.001f, 1e10f, h.t, r, st);
                 if (m.is_hit) {
                     hp = m.p;
                     n = pt_v3f(1.0f, 0.0f, 0.0f);
@@ -490,7 +554,7 @@ static pt_v3 trace_ray_wf(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
     for (int wave = 0; wave < fr->max_depth; ++wave) {       /* renderer.py:313 */
         hit_t h;
         if (st) st->segments++;
-        int hit = traverse_bvh(sc, o, d, 0.001f, 1e10f, &h);  /* intersect_rays :1242 */
+        int hit = traverse(sc, fr->traversal, o, d, 0.001f, 1e10f, &h);  /* intersect_rays :1242 */
         if (!hit) {                                           /* shade_miss_rays :1266 */
             acc = pt_add(acc, pt_mul(thr, bg));
             have = 1;
@@ -502,7 +566,7 @@ static pt_v3 trace_ray_wf(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
         pt_v3 sdir = pt_v3f(0.0f, 0.0f, 0.0f), att = pt_v3f(1.0f, 1.0f, 1.0f), emit = pt_v3f(0.0f, 0.0f, 0.0f);
         pt_v3 hp = h.p;
         if (is_med > 0) {
-            medium_t m = apply_constant_medium(sc, pt, pi, o, d, 0.001f, 1e10f, h.t, r, st);
+            medium_t m = apply_constant_medium(sc, fr->traversal, pt, pi, o, d, 0.001f, 1e10f, h.t, r, st);
             if (m.is_hit) {
                 hp = m.p;
                 sdir = random_unit_vector(r);
@@ -553,7 +617,7 @@ int or_version(void) { return 1; }
 
 int or_render(const or_scene *sc, const or_frame *fr, int variant, float *accum,
               int x0, int y0, int w, int h, int s_begin, int s_count, int threads, or_stats *stats) {
-    if (!sc || !fr || !accum || w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > fr->width || y0 + h > fr->height)
+    if (!sc || !fr || !accum || w <= 0 || (fr->traversal == OR_TRAV_STACKLESS && !sc->bvh_parent && sc->num_bvh_nodes) || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > fr->width || y0 + h > fr->height)
         return -1;
     /* num_bvh_nodes == 0 (empty world, sah_bvh_builder.py:345-355) is legal: the root pop is
        skipped as an invalid node (kernels.py:660) and every path misses */
@@ -577,10 +641,10 @@ int or_render(const or_scene *sc, const or_frame *fr, int variant, float *accum,
     return 0;
 }
 
-int or_traverse(const or_scene *sc, const float *o, const float *d, float tmin, float tmax,
+int or_traverse(const or_scene *sc, int traversal, const float *o, const float *d, float tmin, float tmax,
                 float *t_out, int32_t *type_out, int32_t *idx_out) {
     hit_t h;
-    int hit = traverse_bvh(sc, pt_v3f(o[0], o[1], o[2]), pt_v3f(d[0], d[1], d[2]), tmin, tmax, &h);
+    int hit = traverse(sc, traversal, pt_v3f(o[0], o[1], o[2]), pt_v3f(d[0], d[1], d[2]), tmin, tmax, &h);
     *t_out = h.t; *type_out = hit ? h.type : -1; *idx_out = hit ? h.idx : -1;
     return hit;
 }

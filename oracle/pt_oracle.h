@@ -44,7 +44,15 @@ typedef struct or_scene {
     int32_t num_images;
     const uint8_t *images[OR_MAX_IMAGES];
     int32_t img_w[OR_MAX_IMAGES], img_h[OR_MAX_IMAGES];
+    /* parent pointers of the flattened BVH (sah_bvh_builder.py:398), read by
+       the stackless traversal only */
+    const int32_t *bvh_parent;
 } or_scene;
+
+/* BVH traversal of traverse_bvh (kernels.py:749-759): USE_STACKLESS_TRAVERSAL
+ * (kernels.py:746) False -> traverse_bvh_legacy (:625-742, the reference's
+ * default), True -> traverse_bvh_stackless (:453-597). */
+enum { OR_TRAV_STACK = 0, OR_TRAV_STACKLESS = 1 };
 
 typedef struct or_frame {
     float center[3], pixel00[3], delta_u[3], delta_v[3], defocus_u[3], defocus_v[3];
@@ -53,6 +61,7 @@ typedef struct or_frame {
     int32_t max_depth;
     uint32_t seed;
     int32_t width, height;
+    int32_t traversal;   /* OR_TRAV_* */
 } or_frame;
 
 typedef struct or_stats {
@@ -72,7 +81,7 @@ int or_version(void);
 int or_render(const or_scene *sc, const or_frame *fr, int variant, float *accum,
               int x0, int y0, int w, int h, int s_begin, int s_count, int threads,
               or_stats *stats);
-int or_traverse(const or_scene *sc, const float *o, const float *d, float tmin, float tmax,
+int or_traverse(const or_scene *sc, int traversal, const float *o, const float *d, float tmin, float tmax,
                 float *t_out, int32_t *type_out, int32_t *idx_out);
 /* one path: returns its colour contribution and counters */
 int or_trace_path(const or_scene *sc, const or_frame *fr, int variant, int px, int py, int sample,

@@ -88,6 +88,9 @@ static int to_dev_scene(const ptmi_scene_view* s, DevScene& d) {
   // (kernels.py:719-740); beyond that its silent drops are not reproduced.
   if (s->max_leaf_depth < 0 || s->max_leaf_depth > 62)
     return fail(PTMI_ECAPACITY, "BVH leaf depth %d exceeds 62", s->max_leaf_depth);
+  if (s->num_bvh_nodes != (np > 0 ? 2 * np - 1 : 0))
+    return fail(PTMI_EINVAL, "num_bvh_nodes %d for %d primitives (expected 2N-1)", s->num_bvh_nodes, np);
+  if (s->ref_nodes && !aligned16(s->ref_nodes)) return fail(PTMI_EINVAL, "ref_nodes misaligned");
   std::memset(&d, 0, sizeof d);
   d.nodes = (const float4*)s->nodes;
   d.n_inner = s->n_inner;
@@ -112,6 +115,8 @@ static int to_dev_scene(const ptmi_scene_view* s, DevScene& d) {
   }
   d.perlin_vec = (const float4*)s->perlin_vec;
   d.perlin_perm = s->perlin_perm;
+  d.ref_nodes = (const float4*)s->ref_nodes;
+  d.n_nodes = s->num_bvh_nodes;
   return PTMI_OK;
 }
 
@@ -147,6 +152,9 @@ static int to_dev_frame(const ptmi_frame* f, DevFrame& d) {
   d.band_rows = f->band_rows;
   d.band_stride = f->band_stride;
   d.band_offset = f->band_offset;
+  if (f->traversal != PTMI_TRAV_STACK && f->traversal != PTMI_TRAV_STACKLESS)
+    return fail(PTMI_EINVAL, "unknown traversal %d", f->traversal);
+  d.traversal = f->traversal;
   int32_t n = 0;
   for (int32_t r = 0; r < f->h; ++r)
     if ((r / f->band_rows) % f->band_stride == f->band_offset) ++n;
@@ -155,6 +163,13 @@ static int to_dev_frame(const ptmi_frame* f, DevFrame& d) {
 }
 
 static int32_t stack_needed(const ptmi_scene_view* s) { return s->max_leaf_depth + 1; }
+
+// The stackless traversal walks the reference-layout nodes (ref_nodes).
+static int check_traversal(const DevScene& sc, const DevFrame& fr) {
+  if (fr.traversal == PTMI_TRAV_STACKLESS && sc.n_nodes > 0 && !sc.ref_nodes)
+    return fail(PTMI_EINVAL, "the stackless traversal needs the scene's ref_nodes");
+  return PTMI_OK;
+}
 
 extern "C" {
 
@@ -176,6 +191,7 @@ int ptmi_mk_render(const ptmi_scene_view* scene, const ptmi_frame* frame, float*
   int rc = to_dev_scene(scene, sc);
   if (rc) return rc;
   if ((rc = to_dev_frame(frame, fr))) return rc;
+  if ((rc = check_traversal(sc, fr))) return rc;
   if (!accum) return fail(PTMI_EINVAL, "accum is NULL");
   if (sample_begin < 0 || sample_count < 0) return fail(PTMI_EINVAL, "bad sample range");
   if (sample_count == 0 || fr.n_rows == 0) return PTMI_OK;
@@ -202,6 +218,7 @@ int ptmi_mk_render_ws(const ptmi_scene_view* scene, const ptmi_frame* frame, voi
   int rc = to_dev_scene(scene, sc);
   if (rc) return rc;
   if ((rc = to_dev_frame(frame, fr))) return rc;
+  if ((rc = check_traversal(sc, fr))) return rc;
   if (!accum) return fail(PTMI_EINVAL, "accum is NULL");
   if (sample_begin < 0 || sample_count < 0) return fail(PTMI_EINVAL, "bad sample range");
   const int32_t npix = fr.w * fr.n_rows;
@@ -236,6 +253,7 @@ int ptmi_wf_render(const ptmi_scene_view* scene, const ptmi_frame* frame, void* 
   int rc = to_dev_scene(scene, sc);
   if (rc) return rc;
   if ((rc = to_dev_frame(frame, fr))) return rc;
+  if ((rc = check_traversal(sc, fr))) return rc;
   if (!accum) return fail(PTMI_EINVAL, "accum is NULL");
   if (sample_begin < 0 || sample_count < 0) return fail(PTMI_EINVAL, "bad sample range");
   int32_t npix = fr.w * fr.n_rows;

@@ -39,6 +39,8 @@ struct DevScene {
   int32_t img_offset[PTMI_MAX_IMAGES], img_w[PTMI_MAX_IMAGES], img_h[PTMI_MAX_IMAGES];
   const float4* __restrict__ perlin_vec;
   const int32_t* __restrict__ perlin_perm;
+  const float4* __restrict__ ref_nodes;  // reference-layout nodes (stackless traversal), 3 float4 each
+  int32_t n_nodes;                       // all BVH nodes
 };
 
 struct DevFrame {
@@ -51,6 +53,7 @@ struct DevFrame {
   int32_t x0, y0, w, h;
   int32_t band_rows, band_stride, band_offset;
   int32_t n_rows;  // rows of the window this frame owns (after banding)
+  int32_t traversal;  // PTMI_TRAV_*
 };
 
 __device__ __forceinline__ int32_t leaf_type(int32_t ref) { return (ref >> 28) & 3; }
@@ -709,13 +712,122 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
 }
 
+// ---------------------------------------------------------------- stackless traversal
+// traverse_bvh_stackless (kernels.py:453-597): the reference's alternative
+// traversal, selected by its module constant USE_STACKLESS_TRAVERSAL
+// (kernels.py:746; the frame's PTMI_TRAV_STACKLESS here). It walks the
+// reference's own preorder nodes (ref_nodes, include/ptmi.h) left child
+// first with parent pointers and no stack, one iteration of the reference's
+// loop per step, at most 2 * num_bvh_nodes iterations (:487-491): a node's box
+// is tested against [t_min, closest_t] when the walk enters it (:523), a
+// leaf's primitive right after (:536-571), and the walk climbs back with the
+// `came from` state (:497-520; the reference compares the parent's left child
+// with the node, `side` in ref_nodes is that comparison precomputed). No LDS.
+struct TravSL {
+  pt_v3 inv;
+  float tmin, closest;
+  int32_t best;  // leaf code of the closest hit; 0 = none
+  int32_t node;  // current node index; -1 = the walk has left the root
+  int32_t came;  // -1 entering node, 0 back from its left child, 1 back from its right child
+  int32_t it, max_it;
+#if PTMI_PROBE == 2
+  uint32_t probe;
+#endif
+  __device__ __forceinline__ bool any() const { return best != 0; }
+  __device__ __forceinline__ bool busy() const { return node >= 0 && it < max_it; }
+  __device__ __forceinline__ void init(Stack) {
+    node = -1;
+    it = max_it = 0;
+    best = 0;
+  }
+};
+
+template <int STACK, int SB = kBlock>
+__device__ __forceinline__ void trav_begin(const DevScene& sc, TravSL& tr, Stack, pt_v3 d, pt_v3 o, float tmin,
+                                           float tmax) {
+  (void)o;
+  tr.inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                  fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:478-482 (Q15)
+  tr.tmin = tmin;
+  tr.closest = tmax;
+  tr.best = 0;
+  tr.node = 0;
+  tr.came = -1;
+  tr.it = 0;
+  tr.max_it = 2 * sc.n_nodes;
+}
+
+// One iteration of the reference's while loop (kernels.py:493-595).
+template <int STACK, int SB = kBlock>
+__device__ __forceinline__ void trav_step(const DevScene& sc, const float4*, TravSL& tr, Stack, pt_v3 o, pt_v3 d) {
+  ++tr.it;
+  const float4* nd = sc.ref_nodes + 3 * tr.node;
+  const float4 s0 = nd[0], s1 = nd[1], s2 = nd[2];
+  const int32_t left = __float_as_int(s0.w), right = __float_as_int(s1.w);
+  bool up = false;
+  if (tr.came == 0) {  // back from the left child: the right one next, else climb (:497-510)
+    if (right >= 0) {
+      tr.node = right;
+      tr.came = -1;
+      return;
+    }
+    up = true;
+  } else if (tr.came == 1) {  // back from the right child: climb (:511-520)
+    up = true;
+  } else {
+    // hit_aabb_optimized (kernels.py:601-621) against [t_min, closest_t]
+    const float t0x = (s0.x - o.x) * tr.inv.x, t1x = (s1.x - o.x) * tr.inv.x;
+    const float t0y = (s0.y - o.y) * tr.inv.y, t1y = (s1.y - o.y) * tr.inv.y;
+    const float t0z = (s0.z - o.z) * tr.inv.z, t1z = (s1.z - o.z) * tr.inv.z;
+    const float lo = pt_maxf(pt_maxf(pt_minf(t0x, t1x), pt_minf(t0y, t1y)), pt_maxf(pt_minf(t0z, t1z), tr.tmin));
+    const float hi = pt_minf(pt_minf(pt_maxf(t0x, t1x), pt_maxf(t0y, t1y)), pt_minf(pt_maxf(t0z, t1z), tr.closest));
+    const int32_t code = __float_as_int(s2.y);
+    if (!(hi >= lo)) {
+      up = true;  // :523-533
+    } else if (code != 0) {  // leaf: test its primitive, then climb (:536-571)
+#if PTMI_PROBE == 2
+      tr.probe |= leaf_type(code) == kSphere ? 1 : 2;
+#endif
+      float t;
+      if (hit_leaf(sc, code, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
+        tr.closest = t;
+        tr.best = code;
+      }
+      up = true;
+    } else if (left >= 0) {  // internal: left child first (:572-595)
+      tr.node = left;
+      tr.came = -1;
+    } else if (right >= 0) {
+      tr.node = right;
+      tr.came = -1;
+    } else {
+      up = true;
+    }
+  }
+  if (up) {  // parent >= 0: came = which child this node is; else done
+    const int32_t p = __float_as_int(s2.x);
+    tr.came = __float_as_int(s2.z);
+    tr.node = p;  // -1 at the root
+  }
+}
+
+// Traversal state type by frame.traversal (PTMI_TRAV_*).
+template <int TRAV>
+struct TravOf {
+  typedef Trav T;
+};
+template <>
+struct TravOf<PTMI_TRAV_STACKLESS> {
+  typedef TravSL T;
+};
+
 #ifndef PTMI_TRAV_UNROLL
 #define PTMI_TRAV_UNROLL 3  // pops per loop test in traverse() (wavefront kernels; A/B: 3 +0.5 % C3 / mesh fog, 2 +0.3 %)
 #endif
-template <int STACK, int SB = kBlock>
+template <int STACK, int SB = kBlock, int TRAV = PTMI_TRAV_STACK>
 __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
                                          float& t_out, int32_t& ref_out) {
-  Trav tr;
+  typename TravOf<TRAV>::T tr;
   trav_begin<STACK, SB>(sc, tr, st, d, o, tmin, tmax);
   while (tr.busy()) {
 #pragma unroll

@@ -138,9 +138,11 @@ struct MkWork {
 constexpr int kMkTile = PTMI_MK_BLOCK_WAVES == 4 ? 16 : 8;
 static_assert(PTMI_MK_BLOCK_WAVES == 4 || PTMI_MK_BLOCK_WAVES == 1, "block = 1 or 4 waves");
 
-template <int STACK, bool STAGED>
+template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
-// (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the 4-wave VGPR budget of 128
+// (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the 4-wave VGPR budget of 128.
+// TRAV = PTMI_TRAV_STACKLESS (STACK 1: no stack) walks the reference's
+// stackless traversal instead (TravSL, pt_device.hpp).
 __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   // item) while the stragglers wait with their traversal state kept — instead
   // of the whole wave idling until its longest traversal ends (node steps ran
   // at ~35 % SIMD efficiency that way). 0 = wait for every lane.
-  Trav tr;
+  typename TravOf<TRAV>::T tr;
   tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
   bool hold = false;  // PTMI_MK_HOLD_NOISE: a traced Perlin-textured hit waiting for more of its kind
@@ -546,12 +548,12 @@ hipError_t launch_stage_resolve(const DevFrame& fr, const float* staging, int32_
   return hipGetLastError();
 }
 
-template <int STACK>
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum, int32_t s_begin,
                             int32_t s_count, unsigned long long* counters, hipStream_t stream) {
   dim3 grid((unsigned)((fr.w + kMkTile - 1) / kMkTile), (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile));
   prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, false>), grid, dim3(kMkBlock), 0, stream, sc, fr, accum, s_begin,
+  hipLaunchKernelGGL((mk_render_kernel<STACK, false, TRAV>), grid, dim3(kMkBlock), 0, stream, sc, fr, accum, s_begin,
                      s_count, s_count, (float*)nullptr, counters, MkWork{});
   prof_end(kProfMk, stream);
   return hipGetLastError();
@@ -559,6 +561,8 @@ static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum
 
 hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, float* accum,
                      int32_t s_begin, int32_t s_count, unsigned long long* counters, hipStream_t stream) {
+  if (fr.traversal == PTMI_TRAV_STACKLESS)
+    return launch_mk<1, PTMI_TRAV_STACKLESS>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 16) return launch_mk<16>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 20) return launch_mk<20>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 24) return launch_mk<24>(sc, fr, accum, s_begin, s_count, counters, stream);
@@ -587,7 +591,7 @@ size_t mk_workspace_bytes(int32_t npix, int32_t batch) {  // staging + one 256-B
   return mk_staging_bytes(npix, batch) + 256;
 }
 
-template <int STACK>
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float* staging, float* accum,
                                    int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream) {
   const unsigned tx = (unsigned)((fr.w + kMkTile - 1) / kMkTile), ty = (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile);
@@ -598,7 +602,7 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   hipError_t e0 = hipGetDevice(&dev);
   if (e0 == hipSuccess) e0 = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e0 == hipSuccess)
-    e0 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk_render_kernel<STACK, true>, kMkBlock, 0);
+    e0 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk_render_kernel<STACK, true, TRAV>, kMkBlock, 0);
   if (e0 != hipSuccess) return e0;
   MkWork wk;
   wk.ctl = (int32_t*)((char*)staging + mk_staging_bytes(fr.w * fr.n_rows, nb));
@@ -618,7 +622,7 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   wk.tail_div = (int32_t)(PTMI_MK_TAIL_DIV * waves);
   (void)hipMemsetAsync(wk.ctl, 0, sizeof(int32_t), stream);
   prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
+  hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, nb, staging, counters, wk);
   prof_end(kProfMk, stream);
 #else
@@ -628,7 +632,7 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   const int32_t chunk = (int32_t)((nb + nchunks - 1) / nchunks);
   nchunks = (nb + chunk - 1) / chunk;
   prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, true>), dim3(tx, ty, (unsigned)nchunks), dim3(kMkBlock), 0, stream,
+  hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3(tx, ty, (unsigned)nchunks), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, chunk, staging, counters, MkWork{});
   prof_end(kProfMk, stream);
 #endif
@@ -655,7 +659,9 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
     const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
     float* st = (float*)ws;
     hipError_t e;
-    if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    if (fr.traversal == PTMI_TRAV_STACKLESS)
+      e = launch_mk_staged<1, PTMI_TRAV_STACKLESS>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    else if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 20) e = launch_mk_staged<20>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 24) e = launch_mk_staged<24>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
     else if (stack_needed <= 32) e = launch_mk_staged<32>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);

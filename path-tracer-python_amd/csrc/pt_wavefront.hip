@@ -372,7 +372,7 @@ __device__ __forceinline__ void assign_work(const DevFrame& fr, const WfBufs& wb
 }
 
 // intersect_rays, kernels.py:1242-1263.
-template <int STACK>
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb,
                                                        unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
     pt_v3 o = pt_v3f(a.x, a.y, a.z), d = pt_v3f(a.w, b.x, b.y);
     float t;
     int32_t ref;
-    bool hit = traverse<STACK, kWfBlock>(sc, o, d, kTMin, kTMax, st, t, ref);
+    bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
     h_store(wb.hit + i, make_float2(t, __int_as_float(hit ? ref : kMissRef)));
   }
   if (counters) block_flush(n_live, lds_stack, counters + 0);
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
 // Constant-medium rays: exit traversal + free flight (apply_constant_medium,
 // kernels.py:365-450) and the volume branch of shade_and_scatter
 // (kernels.py:1326-1357). Work index j runs over the concatenated shard segments.
-template <int STACK>
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
 #ifndef PTMI_WF_MEDIUM_MIN_WAVES
 #define PTMI_WF_MEDIUM_MIN_WAVES 4  // <= 128 VGPRs: with the deferred shading list it needs 131 otherwise (3 waves/SIMD)
 #endif
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
       const float t_entry = h.x;
       float te;
       int32_t rex;
-      const bool hx = traverse<STACK, kWfBlock>(sc, ray.o, ray.d, t_entry + 0.0001f, kTMax, st, te, rex);
+      const bool hx = traverse<STACK, kWfBlock, TRAV>(sc, ray.o, ray.d, t_entry + 0.0001f, kTMax, st, te, rex);
       const Mat m = load_mat(sc, mat_index(sc, ref));
       Item it = decode_item(fr, wb, ray.item);
       Rng r{path_key(fr, wb, it), ray.ctr};
@@ -696,7 +696,7 @@ static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must 
 // One batch: generate on the caller's stream, fork the pipes, run each pipe's
 // intersect -> shade -> medium loop on its own stream until its slots have all
 // retired, join, resolve.
-template <int STACK>
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs* wbs, float* accum, int32_t batch,
                            unsigned long long* counters, hipStream_t stream, const PipeStreams& ps) {
 #ifdef PTMI_WF_NOCOUNT
@@ -745,13 +745,13 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
         if (!live[p]) continue;
         const WfBufs& wb = wbs[p];
         prof_begin(kProfWfIntersect, st[p]);
-        hipLaunchKernelGGL(wf_intersect<STACK>, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        hipLaunchKernelGGL((wf_intersect<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
         prof_end(kProfWfIntersect, st[p]);
         prof_begin(kProfWfShade, st[p]);
         hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
         prof_end(kProfWfShade, st[p]);
         prof_begin(kProfWfMedium, st[p]);
-        hipLaunchKernelGGL(wf_medium<STACK>, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        hipLaunchKernelGGL((wf_medium<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
         prof_end(kProfWfMedium, st[p]);
       }
     }
@@ -872,7 +872,8 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
       wb.s_begin = s_begin + b0;
     }
     hipError_t e;
-    if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    if (fr.traversal == PTMI_TRAV_STACKLESS) e = wf_batch<1, PTMI_TRAV_STACKLESS>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wbs, accum, nb, counters, stream, *ps);

@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PTMI_LIB') or os.path.join(_HERE, '_lib', 'libptmi.so')  # PTMI_LIB: A/B builds
-ABI_VERSION = 4  # PTMI_ABI_VERSION of include/ptmi.h
+ABI_VERSION = 5  # PTMI_ABI_VERSION of include/ptmi.h
 MAX_IMAGES = 16
 NUM_COUNTERS = 4
 
@@ -30,6 +30,7 @@ class SceneView(C.Structure):
         ('img_offset', C.c_int32 * MAX_IMAGES), ('img_w', C.c_int32 * MAX_IMAGES),
         ('img_h', C.c_int32 * MAX_IMAGES),
         ('perlin_vec', C.c_void_p), ('perlin_perm', C.c_void_p),
+        ('ref_nodes', C.c_void_p), ('num_bvh_nodes', C.c_int32),
     ]
 
 
@@ -42,7 +43,14 @@ class Frame(C.Structure):
     _fields_ = [('cam', Camera), ('bg', f3), ('max_depth', C.c_int32), ('seed', C.c_uint32),
                 ('width', C.c_int32), ('height', C.c_int32),
                 ('x0', C.c_int32), ('y0', C.c_int32), ('w', C.c_int32), ('h', C.c_int32),
-                ('band_rows', C.c_int32), ('band_stride', C.c_int32), ('band_offset', C.c_int32)]
+                ('band_rows', C.c_int32), ('band_stride', C.c_int32), ('band_offset', C.c_int32),
+                ('traversal', C.c_int32)]
+
+
+# BVH traversal of a frame (ptmi_frame.traversal): the reference's
+# traverse_bvh_legacy (default) or traverse_bvh_stackless, switched in the
+# reference by USE_STACKLESS_TRAVERSAL (kernels.py:746)
+TRAVERSALS = {'stack': 0, 'stackless': 1}
 
 
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',

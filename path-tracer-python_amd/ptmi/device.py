@@ -67,6 +67,7 @@ class DeviceScene:
         self.t_texels = up(layout.texels.view(np.int32))
         self.t_pvec = up(layout.perlin_vec)
         self.t_perm = up(layout.perlin_perm)
+        self.t_ref_nodes = up(layout.ref_nodes) if layout.ref_nodes is not None else None
         v = _lib.SceneView()
         v.nodes = self.t_nodes.data_ptr()
         v.n_inner = layout.n_inner
@@ -88,6 +89,10 @@ class DeviceScene:
             v.img_h[k] = layout.img_h[k]
         v.perlin_vec = self.t_pvec.data_ptr()
         v.perlin_perm = self.t_perm.data_ptr()
+        if self.t_ref_nodes is not None:
+            v.ref_nodes = self.t_ref_nodes.data_ptr()
+        v.num_bvh_nodes = layout.num_bvh_nodes if layout.ref_nodes is not None else \
+            (2 * (layout.n_inner + 1) - 1 if layout.num_spheres + layout.num_quads + layout.num_triangles else 0)
         self.view = v
         _lib.check(_lib.load().ptmi_scene_check(C.byref(v)), 'ptmi_scene_check')
 
@@ -96,10 +101,15 @@ class DeviceScene:
         return cls(sa, device)
 
 
-def make_frame(cam, bg, max_depth, seed, width, height, window=None, band=(1, 1, 0)):
+def make_frame(cam, bg, max_depth, seed, width, height, window=None, band=(1, 1, 0), traversal='stack'):
     """ptmi_frame from camera upload values (dict of f32 3-vectors or an
-    object with the reference camera's attributes)."""
+    object with the reference camera's attributes). ``traversal``: 'stack'
+    (traverse_bvh_legacy, the reference's default) or 'stackless'
+    (traverse_bvh_stackless, its USE_STACKLESS_TRAVERSAL = True)."""
     f = _lib.Frame()
+    if traversal not in _lib.TRAVERSALS:
+        raise _lib.PtmiError(f'unknown traversal {traversal!r} (one of {sorted(_lib.TRAVERSALS)})')
+    f.traversal = _lib.TRAVERSALS[traversal]
     vals = cam if isinstance(cam, dict) else camera_upload(cam)
     get = vals.__getitem__
     for k, fld in (('center', 'center'), ('pixel00', 'pixel00'), ('delta_u', 'delta_u'), ('delta_v', 'delta_v'),

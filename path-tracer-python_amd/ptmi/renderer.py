@@ -24,6 +24,12 @@ import numpy as np
 from . import _lib, bvh as bvh_mod, core, device, scene_compiler
 from .scene_data import SceneArrays
 
+# kernels.py:746: the reference's switch between its front-to-back stack
+# traversal (False, its default) and its parent-pointer stackless traversal.
+# Read when a renderer uploads its camera; the per-renderer attribute
+# `use_stackless_traversal` overrides it.
+USE_STACKLESS_TRAVERSAL = False
+
 
 class MI355XRenderer:
     def __init__(self, world, cam, img_path: str, seed: int = 0, samples_per_launch: int = 0, device_id=None):
@@ -39,6 +45,7 @@ class MI355XRenderer:
         self.max_depth = 50
         self.background_color = (0.70, 0.80, 1.00)
         self.seed = int(seed)
+        self.use_stackless_traversal = USE_STACKLESS_TRAVERSAL
         # launches per progress report: one launch renders many samples (path regeneration)
         self.samples_per_launch = int(samples_per_launch)
         device.require_gpu()
@@ -68,7 +75,8 @@ class MI355XRenderer:
     def _upload_camera(self):
         """renderer.py:230-247: camera + background + max_depth as f32/i32."""
         W, H = self.cam.img_width, self.cam.img_height
-        self.frame = device.make_frame(self.cam, self.background_color, self.max_depth, self.seed, W, H)
+        self.frame = device.make_frame(self.cam, self.background_color, self.max_depth, self.seed, W, H,
+                                       traversal='stackless' if self.use_stackless_traversal else 'stack')
         if tuple(self.accum.shape[:2]) != (H, W):
             import torch
             self.accum = torch.zeros((H, W, 3), dtype=torch.float32, device=self.dscene.device)

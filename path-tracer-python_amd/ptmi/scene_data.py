@@ -207,6 +207,13 @@ class DeviceLayout:
     # device primitive k of type t is the reference's primitive prim_perm[t][k]
     # (types indexed sphere 0, triangle 1, quad 2; identity unless leaf_order)
     prim_perm: tuple = ()
+    # the reference's own nodes for the stackless traversal (include/ptmi.h
+    # ref_nodes): (num_bvh_nodes, 12) f32
+    ref_nodes: np.ndarray = None
+
+    @property
+    def num_bvh_nodes(self):
+        return 0 if self.ref_nodes is None else int(self.ref_nodes.shape[0])
 
     @property
     def n_inner(self):
@@ -214,7 +221,8 @@ class DeviceLayout:
 
     def nbytes(self):
         return sum(int(a.nbytes) for a in (self.nodes, self.spheres, self.quads, self.tris, self.mats,
-                                              self.texels, self.perlin_vec, self.perlin_perm))
+                                              self.texels, self.perlin_vec, self.perlin_perm)
+                   if a is not None) + (0 if self.ref_nodes is None else int(self.ref_nodes.nbytes))
 
 
 def _pack_mats(m, n):
@@ -284,6 +292,33 @@ def leaf_order_perm(bvh, counts):
     return tuple(perm)
 
 
+def ref_layout_nodes(bvh, codes):
+    """The reference's flattened nodes (fields.py:52-63, in its preorder) for
+    the stackless traversal (traverse_bvh_stackless, kernels.py:453-597):
+    12 f32 per node {min.xyz, left | max.xyz, right | parent, leaf code, side,
+    0} (i32 bits). ``codes``: the device leaf code of every leaf (0 for
+    internal nodes). ``side`` precomputes the reference's climb test
+    ``0 if parent_node.left_child == node_idx else 1`` (kernels.py:506-507)."""
+    left, right, parent = bvh['bvh_left_child'], bvh['bvh_right_child'], bvh['bvh_parent']
+    n = left.shape[0]
+    out = np.zeros((n, 12), np.float32)
+    if n == 0:
+        return out
+    if np.any(parent[1:] < 0) or np.any(parent >= n) or parent[0] >= 0:
+        raise ValueError('BVH parent pointers: only the root (node 0) may lack a parent')
+    side = np.zeros(n, np.int32)
+    has = parent >= 0
+    side[has] = (left[parent[has]] != np.nonzero(has)[0]).astype(np.int32)
+    out[:, 0:3] = bvh['bvh_bbox_min']
+    out[:, 3] = left.astype(np.int32).view(np.float32)
+    out[:, 4:7] = bvh['bvh_bbox_max']
+    out[:, 7] = right.astype(np.int32).view(np.float32)
+    out[:, 8] = parent.astype(np.int32).view(np.float32)
+    out[:, 9] = np.asarray(codes, np.int32).view(np.float32)
+    out[:, 10] = side.view(np.float32)
+    return out
+
+
 def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True) -> DeviceLayout:
     """Reference-layout arrays -> include/ptmi.h device layout. ``node_bytes``
     is the library's node stride (ptmi_node_bytes()): 80 for one child record
@@ -347,6 +382,7 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
                 inner = cidx[ch] >= 0
                 pk[inner, k * NODE_FLOATS:(k + 1) * NODE_FLOATS] = nodes[cidx[ch[inner]]]
         nodes = pk
+    ref_nodes = ref_layout_nodes(b, np.where(is_leaf, codes, 0).astype(np.int32))
     if n:
         root_ref = int(refs[0])
         root_min, root_max = bmin[0].copy(), bmax[0].copy()
@@ -392,7 +428,7 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
     if pperm.min() < 0 or pperm.max() > 255:
         raise ValueError('Perlin permutation out of range')
     return DeviceLayout(nodes, root_ref, root_min, root_max, max_leaf_depth, spheres, quads, tris, mats,
-                        texels, offs, ws, hs, pv, pperm, ns, nq, nt, perm)
+                        texels, offs, ws, hs, pv, pperm, ns, nq, nt, perm, ref_nodes)
 
 
 def compile_world(world, perlin_tables=None):

@@ -50,11 +50,12 @@ def scene_inputs(name, width):
     return fixture(name), sd.fixture_camera(name, width), BG[name]
 
 
-def oracle_render(name, width, variant, window, s_begin, s_count, seed=0, max_depth=50, threads=0, acc=None):
+def oracle_render(name, width, variant, window, s_begin, s_count, seed=0, max_depth=50, threads=0, acc=None,
+                  traversal='stack'):
     import oracle
     sa, cam, bg = scene_inputs(name, width)
     W, H = cam['width'], cam['height']
-    fr = oracle.make_frame(cam, bg, max_depth, seed, W, H)
+    fr = oracle.make_frame(cam, bg, max_depth, seed, W, H, traversal)
     if acc is None:
         acc = np.zeros((H, W, 3), np.float32)
     stats = oracle.render(oracle.OracleScene(sa), fr, variant, acc, window, s_begin, s_count, threads)
@@ -62,14 +63,14 @@ def oracle_render(name, width, variant, window, s_begin, s_count, seed=0, max_de
 
 
 def gpu_render(name, width, variant, window, s_begin, s_count, seed=0, max_depth=50, band=(1, 1, 0),
-               chunks=None, integ=None):
+               chunks=None, integ=None, traversal='stack'):
     import torch
     from ptmi import device
     sa, cam, bg = scene_inputs(name, width)
     W, H = cam['width'], cam['height']
     if integ is None:
         integ = device.Integrator(device.DeviceScene.from_arrays(sa))
-    fr = device.make_frame(cam, bg, max_depth, seed, W, H, window, band)
+    fr = device.make_frame(cam, bg, max_depth, seed, W, H, window, band, traversal=traversal)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
     integ.reset_counters()
     chunks = chunks or [(s_begin, s_count)]

@@ -12,8 +12,9 @@ from parity_helpers import compare, oracle_render
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize('traversal', ['stack', 'stackless'])
 @pytest.mark.parametrize('method,variant', [('render', 'mk'), ('render_wavefront', 'wf')])
-def test_renderer_end_to_end(tmp_path, method, variant):
+def test_renderer_end_to_end(tmp_path, method, variant, traversal):
     from ptmi import scenes
     from ptmi.renderer_factory import RendererFactory
     random.seed(1234)
@@ -24,10 +25,11 @@ def test_renderer_end_to_end(tmp_path, method, variant):
     r = RendererFactory.create('taichi', sc.world, sc.cam, out)
     r.background_color = sc.background
     r.max_depth = sc.max_depth
+    r.use_stackless_traversal = traversal == 'stackless'  # kernels.py:746, read at render time
     getattr(r, method)(enable_preview=False)
     assert os.path.exists(out)
     g = r.accum.cpu().numpy()
-    o, _ = oracle_render('wavefront_comparison', 400, variant, (0, 0, 400, 225), 0, 3)
+    o, _ = oracle_render('wavefront_comparison', 400, variant, (0, 0, 400, 225), 0, 3, traversal=traversal)
     linf, exact = compare(g, o, 3)
     assert linf <= 1e-4 and exact >= 0.999
     assert r.num_spheres == 41 and r.num_bvh_nodes == 81

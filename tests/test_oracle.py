@@ -77,8 +77,11 @@ def brute_force(sa, o, d, tmin=np.float32(0.001), tmax=np.float32(1e10)):
     return best_t, best
 
 
+@pytest.mark.parametrize('traversal', ['stack', 'stackless'])
 @pytest.mark.parametrize('name', ['wavefront_comparison', 'cornell_smoke', 'coverage'])
-def test_traversal_matches_brute_force(name):
+def test_traversal_matches_brute_force(name, traversal):
+    """Both of the reference's traversals (traverse_bvh_legacy, kernels.py:625,
+    and traverse_bvh_stackless, :453) find the brute-force closest hit."""
     sa, cam, _ = scene_inputs(name, 800 if name != 'coverage' else 160)
     osc = oracle.OracleScene(sa)
     rng = np.random.default_rng(5)
@@ -89,7 +92,7 @@ def test_traversal_matches_brute_force(name):
         o = cam['center'] + rng.normal(0, 0.5, 3).astype(np.float32)
         d = (cam['pixel00'] + rng.uniform(0, cam['width']) * cam['delta_u'] + rng.uniform(0, cam['height']) * cam['delta_v']
              - o).astype(np.float32)
-        hit, t, ty, ix = oracle.traverse(osc, o, d)
+        hit, t, ty, ix = oracle.traverse(osc, o, d, traversal=traversal)
         tri_hits += bool(hit and ty == 1)
         bt, (bty, bix) = brute_force(sa, o.astype(np.float32), d)
         if bty < 0:
@@ -145,3 +148,26 @@ def test_oracle_deterministic_and_window_local():
     full, _ = oracle_render('vol2_final_scene', 64, 'mk', (0, 0, 64, 64), 0, 3)
     assert np.array_equal(full[8:24, 8:24], a[8:24, 8:24])
     assert not a[:8].any()
+
+
+def test_stackless_traversal_iterations_cover_a_full_walk():
+    """kernels.py:487-491 caps the stackless loop at 2 * num_bvh_nodes
+    iterations; a walk of every node takes 3 per internal node + 1 per leaf =
+    4L - 3 < 4L - 2, so the cap never cuts a traversal short: a ray from inside
+    the root box that must visit every node still finds the brute-force hit."""
+    sa, cam, _ = scene_inputs('wavefront_comparison', 800)
+    osc = oracle.OracleScene(sa)
+    c = (sa.bvh['bvh_bbox_min'][0] + sa.bvh['bvh_bbox_max'][0]) * np.float32(0.5)
+    for d in (np.array([0.3, -1.0, 0.2], np.float32), np.array([0.0, 1.0, 0.0], np.float32)):
+        a = oracle.traverse(osc, c, d, traversal='stack')
+        b = oracle.traverse(osc, c, d, traversal='stackless')
+        assert a[:2] == b[:2]
+
+
+def test_stackless_render_matches_stack_statistically():
+    """USE_STACKLESS_TRAVERSAL changes only the leaf visiting order (left first,
+    kernels.py:572-577): the closest hit differs only on exact ties, so the
+    two renders agree on almost every pixel."""
+    a, _ = oracle_render('vol2_final_scene', 64, 'mk', (0, 0, 64, 64), 0, 2)
+    b, _ = oracle_render('vol2_final_scene', 64, 'mk', (0, 0, 64, 64), 0, 2, traversal='stackless')
+    assert np.mean(np.all(a == b, axis=2)) > 0.99

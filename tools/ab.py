@@ -1,5 +1,5 @@
 """A/B timing of one libptmi build (PTMI_LIB=...) on one workload (not product).
-usage: ab.py VARIANT(mk|mkd|wf) SPP REPS [SCENE WIDTH]"""
+usage: ab.py VARIANT(mk|mkd|wf|mksl|wfsl) SPP REPS [SCENE WIDTH]  (sl: stackless traversal)"""
 import os, sys, time, json
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
 sys.path[:0] = [os.path.join(ROOT, 'path-tracer-python_amd'), ROOT]
@@ -17,9 +17,9 @@ def main():
     sa, cam, bg, _ = bench.load_workload(scene, width)
     W, H = cam['width'], cam['height']
     integ = device.Integrator(device.DeviceScene.from_arrays(sa))
-    fr = device.make_frame(cam, bg, 50, 0, W, H)
+    fr = device.make_frame(cam, bg, 50, 0, W, H, traversal='stackless' if variant.endswith('sl') else 'stack')
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
-    f = {'mk': integ.render_mk, 'wf': integ.render_wf,
+    f = {'mk': integ.render_mk, 'wf': integ.render_wf, 'mksl': integ.render_mk, 'wfsl': integ.render_wf,
          'mkd': lambda *a: integ.render_mk(*a, staged=False)}[variant]
     f(fr, acc, 0, 4); torch.cuda.synchronize()
     best = 1e9
