@@ -42,7 +42,7 @@ def main():
         'wave_issue_frac': round(v['SQ_ACTIVE_INST_ANY'] / v['SQ_WAVE_CYCLES'], 4),
         'valu_insts': v['SQ_INSTS_VALU'],
         'kernel_ms': round(cycles / 2.4e6, 3),
-        'source': 'profiles/r01/pmc_latency/mk_{a,b,c}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
+        'source': os.path.relpath(d, ROOT) + '/mk_{a,b,c}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
                   'tools/ab.py mk 32 1, one 32-spp launch); tools/pmc_valu.py',
     }
     path = os.path.join(ROOT, 'profiles', 'valu.json')
