@@ -36,6 +36,10 @@ def test_struct_layouts_match_header():
     assert C.sizeof(_lib.Camera) == 19 * 4
     assert _lib.Frame.band_offset.offset == C.sizeof(_lib.Camera) + 4 * (3 + 1 + 1 + 2 + 4 + 2)
     assert _lib.SceneView.perlin_perm.offset > _lib.SceneView.img_h.offset
+    # ABI v5 additions sit at the ends of both structs
+    assert _lib.Frame.traversal.offset == _lib.Frame.band_offset.offset + 4
+    assert _lib.SceneView.num_bvh_nodes.offset == _lib.SceneView.ref_nodes.offset + 8
+    assert C.sizeof(_lib.SceneView) == _lib.SceneView.num_bvh_nodes.offset + 8  # padded to 8
 
 
 def make_frame(**kw):
@@ -61,6 +65,17 @@ def test_frame_validation_errors(kw, msg):
     assert msg in lib.ptmi_last_error().decode()
 
 
+def test_unknown_traversal_is_rejected():
+    lib = _lib.load()
+    f = make_frame()
+    f.traversal = 2
+    assert lib.ptmi_clear(C.byref(f), C.c_void_p(16), None) == _lib.PTMI_EINVAL
+    assert 'traversal' in lib.ptmi_last_error().decode()
+    with pytest.raises(_lib.PtmiError):
+        make_frame(traversal='restart-trail')
+    assert make_frame(traversal='stackless').traversal == 1 and make_frame().traversal == 0
+
+
 def test_scene_validation_errors():
     lib = _lib.load()
     v = _lib.SceneView()
@@ -72,6 +87,15 @@ def test_scene_validation_errors():
     v.max_leaf_depth = 63
     v.nodes = v.spheres = v.mats = v.perlin_vec = v.perlin_perm = 16
     assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_ECAPACITY
+    v.max_leaf_depth = 2
+    v.num_bvh_nodes = 4  # 3 primitives: 2N - 1 = 5 nodes
+    assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_EINVAL
+    assert 'num_bvh_nodes' in lib.ptmi_last_error().decode()
+    v.num_bvh_nodes = 5
+    v.ref_nodes = 24  # not 16-byte aligned
+    assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_EINVAL
+    v.ref_nodes = None  # optional: only the stackless traversal reads it
+    assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_OK
 
 
 def test_render_rejects_bad_arguments_before_touching_device():
