@@ -462,6 +462,56 @@ __device__ __forceinline__ bool noise_shaded(uint32_t flags) {
   return tx == 3u && (mt == 0u || mt == 4u);
 }
 
+#ifndef PTMI_WF_SORT
+#define PTMI_WF_SORT 0
+#endif
+constexpr int kWfWaves = kWfBlock / 64;
+
+// PTMI_WF_SORT: wf_shade writes the continuing rays of its 256-slot chunk back
+// sorted by direction octant (stable: slot order within an octant), into the
+// chunk's slots that held miss/surface rays, and marks the rest of those slots
+// as waiting for work; medium and deferred-noise slots stay where they are.
+// A ray record is self-contained (item, random-draw counter, depth and wave
+// count travel with it) and paths never interact, so which slot carries a
+// ray changes nothing in the results; the next wf_intersect's waves then hold
+// rays of one octant from nearby pixel squares. Block-uniform (two barriers).
+// A/B on MI355X (parity-identical): -8 % C3 and mesh fog: a wave's rays come
+// from one pixel square, and that origin coherence is worth more than the
+// direction coherence the sort buys (profiles/r02/ab/ab_wf_octant_sort.log).
+__device__ __forceinline__ void sorted_writeback(const Queue& q, int32_t i, bool ended, bool go, const Ray& cont,
+                                                 int32_t* sort_pos, int32_t (*sort_cnt)[8], int32_t* sort_nsurf) {
+  const int w = (int)(threadIdx.x >> 6);
+  const bool surf = ended || go;  // a miss / surface slot this pass rewrites
+  const int key = go ? ((cont.d.x < 0.0f ? 1 : 0) | (cont.d.y < 0.0f ? 2 : 0) | (cont.d.z < 0.0f ? 4 : 0)) : 0;
+  const unsigned long long ms = __ballot(surf);
+  unsigned long long mine = 0ull;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const unsigned long long m = __ballot(go && key == k);
+    if (lane_id() == 0) sort_cnt[w][k] = (int32_t)__popcll(m);
+    if (go && key == k) mine = m;
+  }
+  if (lane_id() == 0) sort_nsurf[w] = (int32_t)__popcll(ms);
+  __syncthreads();
+  int32_t soff = 0, n_go = 0, boff = 0;
+  for (int v = 0; v < kWfWaves; ++v) soff += v < w ? sort_nsurf[v] : 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    for (int v = 0; v < kWfWaves; ++v) {
+      const int32_t c = sort_cnt[v][k];
+      n_go += c;
+      boff += (k < key || (k == key && v < w)) ? c : 0;
+    }
+  const int32_t srank = soff + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(ms >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ms, 0u));
+  if (surf) sort_pos[srank] = i;
+  __syncthreads();
+  if (go) {
+    const int32_t r = boff + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    store_ray(q, sort_pos[r], cont);
+  }
+  if (surf && srank >= n_go) s_store(reinterpret_cast<uint32_t*>(q.c + i) + 1, kPending);
+}
+
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
 // medium-boundary hits go to their shard's medium queue segment.
 __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
@@ -471,6 +521,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
   __shared__ unsigned int tally;
+#if PTMI_WF_SORT
+  __shared__ int32_t sort_pos[kWfBlock];
+  __shared__ int32_t sort_cnt[kWfWaves][8];
+  __shared__ int32_t sort_nsurf[kWfWaves];
+#endif
   uint32_t n_ended = 0;
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < wb.capacity; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
@@ -504,7 +559,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, W
     const int32_t nslot = wave_ticket(to_noise, ctl_noise(wb, shard));
     if (to_noise) s_store(wb.medq + shard * wb.medseg + wb.medseg - 1 - nslot, i);
 #endif
+#if PTMI_WF_SORT
+    sorted_writeback(q, i, ended, go, cont, sort_pos, sort_cnt, sort_nsurf);
+#else
     finish_lane(wb, i, ended, go, cont);
+#endif
     n_ended += ended ? 1u : 0u;
   }
   if (counters) block_flush(n_ended, &tally, counters + 2);
