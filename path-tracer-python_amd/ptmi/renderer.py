@@ -14,6 +14,14 @@ renderer owns its device buffers (the reference's are module globals), the
 random stream is keyed by (seed, pixel, sample) so ``render_sample(i)``
 renders sample i deterministically, and the preview window is not opened
 (Tk GUI is out of scope): ``enable_preview`` is accepted and ignored.
+
+Checkpoint / resume (the reference has none: its progressive accumulation
+lives only in accum_buffer, renderer.py:405-442):
+``save_checkpoint(path)`` writes the accumulator, the next sample index and
+the render state; ``load_checkpoint(path)`` followed by ``render(resume=True)``
+finishes the remaining samples. Samples are keyed by (seed, pixel, sample) and
+added in sample order, so the resumed image is bit-identical to an
+uninterrupted render.
 """
 from __future__ import annotations
 
@@ -46,6 +54,10 @@ class MI355XRenderer:
         self.background_color = (0.70, 0.80, 1.00)
         self.seed = int(seed)
         self.use_stackless_traversal = USE_STACKLESS_TRAVERSAL
+        # periodic checkpoints during render(): every `checkpoint_every` progress chunks
+        self.checkpoint_path = None
+        self.checkpoint_every = 1
+        self._resume_state = None
         # launches per progress report: one launch renders many samples (path regeneration)
         self.samples_per_launch = int(samples_per_launch)
         device.require_gpu()
@@ -101,14 +113,21 @@ class MI355XRenderer:
         ``sample`` of the counter-based stream, megakernel."""
         self.integrator.render_mk(self.frame, self.accum, int(sample), 1)
 
-    def _run(self, render_fn, label):
+    def _run(self, render_fn, label, resume=False):
         import torch
         self._upload_camera()
         spp = int(self.cam.samples_per_pixel)
         t0 = time.time()
-        render_fn(self.frame, self.accum, 0, 1)  # warm-up sample, then cleared (renderer.py:381-385)
-        torch.cuda.synchronize(self.dscene.device)
-        self.clear_accumulation_buffer()
+        if resume:  # continue a loaded checkpoint: no warm-up, keep the accumulator
+            if self._resume_state is None:
+                raise ValueError('render(resume=True) needs load_checkpoint() first')
+            self._check_resume_state()
+        else:
+            render_fn(self.frame, self.accum, 0, 1)  # warm-up sample, then cleared (renderer.py:381-385)
+            torch.cuda.synchronize(self.dscene.device)
+            self.clear_accumulation_buffer()
+            self.current_sample = 0
+        self._resume_state = None
         self.integrator.reset_counters()
         torch.cuda.synchronize(self.dscene.device)
         self.timing['kernel_warmup'] = time.time() - t0
@@ -117,7 +136,7 @@ class MI355XRenderer:
         print(f'Spheres: {self.num_spheres} | BVH Nodes: {self.num_bvh_nodes}')
         per = self.samples_per_launch or max(1, spp // 20)  # ~20 progress reports, like renderer.py:402
         self.render_start_time = time.time()
-        done = 0
+        done = self.current_sample
         while done < spp:
             n = min(per, spp - done)
             t = time.time()
@@ -130,16 +149,69 @@ class MI355XRenderer:
             pps = self.cam.img_width * self.cam.img_height * n / dt if dt > 0 else 0.0
             print(f'{done:5d}/{spp} ({100.0 * done / spp:5.1f}%) | {dt * 1e3 / n:7.2f} ms/sample | '
                   f'{pps / 1e6:8.2f} Msamples/s')
+            if self.checkpoint_path and done < spp and (done // per) % max(1, self.checkpoint_every) == 0:
+                self.save_checkpoint(self.checkpoint_path)
         self.write_image()
         self.print_statistics()
 
-    def render(self, enable_preview: bool = True):
-        """Megakernel render of cam.samples_per_pixel samples (renderer.py:361-434)."""
-        self._run(self.integrator.render_mk, 'megakernel')
+    def render(self, enable_preview: bool = True, resume: bool = False):
+        """Megakernel render of cam.samples_per_pixel samples (renderer.py:361-434).
+        resume=True continues from a load_checkpoint() state."""
+        self._run(self.integrator.render_mk, 'megakernel', resume)
 
-    def render_wavefront(self, enable_preview: bool = True):
+    def render_wavefront(self, enable_preview: bool = True, resume: bool = False):
         """Wavefront render (renderer.py:249-359)."""
-        self._run(self.integrator.render_wf, 'wavefront')
+        self._run(self.integrator.render_wf, 'wavefront', resume)
+
+    # ------------------------------------------------------- checkpoint/resume
+    # what must match for a checkpoint to continue this render exactly
+    _STATE_KEYS = ('seed', 'max_depth', 'background', 'traversal', 'width', 'height', 'camera', 'scene')
+
+    def _render_state(self):
+        import hashlib
+        lay = self.dscene.layout
+        h = hashlib.sha256()
+        for a in (lay.nodes, lay.spheres, lay.quads, lay.tris, lay.mats, lay.texels, lay.perlin_vec, lay.perlin_perm):
+            h.update(np.ascontiguousarray(a).tobytes())
+        f = self.frame
+        cam = np.array([list(f.cam.center), list(f.cam.pixel00), list(f.cam.delta_u), list(f.cam.delta_v),
+                        list(f.cam.defocus_u), list(f.cam.defocus_v), [f.cam.defocus_angle, 0.0, 0.0]], np.float32)
+        return {'seed': np.int64(f.seed), 'max_depth': np.int64(f.max_depth),
+                'background': np.array(list(f.bg), np.float32), 'traversal': np.int64(f.traversal),
+                'width': np.int64(f.width), 'height': np.int64(f.height), 'camera': cam,
+                'scene': np.array(h.hexdigest())}
+
+    def save_checkpoint(self, path):
+        """Write the accumulator and the next sample index (plain arrays, npz)."""
+        import torch
+        torch.cuda.synchronize(self.dscene.device)
+        st = self._render_state()
+        np.savez(path, accum=self.accum.cpu().numpy(), next_sample=np.int64(self.current_sample), **st)
+
+    def load_checkpoint(self, path):
+        """Load a save_checkpoint() file into this renderer; render(resume=True)
+        then renders samples next_sample .. cam.samples_per_pixel - 1. The
+        render state (scene arrays, camera, seed, max_depth, background,
+        traversal) is checked when the render resumes, after the
+        render-time attributes have been applied."""
+        import torch
+        with np.load(path, allow_pickle=False) as z:
+            state = {k: z[k].copy() for k in self._STATE_KEYS}
+            acc = z['accum'].copy()
+            nxt = int(z['next_sample'])
+        if acc.dtype != np.float32 or acc.ndim != 3 or acc.shape[2] != 3:
+            raise ValueError(f'checkpoint accumulator has shape {acc.shape} / {acc.dtype}')
+        self.accum = torch.from_numpy(acc).to(self.dscene.device)
+        self.current_sample = nxt
+        self._resume_state = state
+
+    def _check_resume_state(self):
+        cur = self._render_state()
+        for k in self._STATE_KEYS:
+            if not np.array_equal(cur[k], self._resume_state[k]):
+                raise ValueError(f'checkpoint was written for another render: {k} differs')
+        if tuple(self.accum.shape) != (int(cur['height']), int(cur['width']), 3):
+            raise ValueError('checkpoint accumulator does not match the image size')
 
     # ----------------------------------------------------------------- output
     def image_u8(self, sample_count=None):

@@ -100,3 +100,59 @@ def test_interactive_viewer_headless(tmp_path):
     r3.render(enable_preview=False)
     assert np.array_equal(v.accum.cpu().numpy(), r3.accum.cpu().numpy())
     assert not np.array_equal(r3.accum.cpu().numpy(), r.accum.cpu().numpy())
+
+
+def _smoke_renderer(spp, out='/dev/null'):
+    from ptmi import scenes
+    from ptmi.renderer import TaichiRenderer
+    random.seed(1234)
+    sc = scenes.cornell_smoke()
+    sc.cam.img_width = 64
+    sc.cam.samples_per_pixel = spp
+    r = TaichiRenderer(sc.world, sc.cam, out)
+    r.background_color = sc.background
+    r.samples_per_launch = 2
+    return r
+
+
+def test_checkpoint_resume_is_bit_identical(tmp_path):
+    """SURVEY.md §5 checkpoint/resume: a render stopped after 4 of 6 samples,
+    saved, loaded into a new renderer and resumed equals the uninterrupted
+    6-sample render bit for bit (samples keyed by (seed, pixel, sample),
+    accumulated in sample order)."""
+    full = _smoke_renderer(6)
+    full.render()
+    ref = full.accum.cpu().numpy()
+    part = _smoke_renderer(4)
+    part.render()
+    ck = str(tmp_path / 'ck.npz')
+    part.save_checkpoint(ck)
+    res = _smoke_renderer(6, str(tmp_path / 'resumed.png'))
+    res.load_checkpoint(ck)
+    assert res.current_sample == 4
+    res.render(resume=True)
+    assert res.current_sample == 6
+    assert np.array_equal(res.accum.cpu().numpy(), ref)
+    assert os.path.exists(tmp_path / 'resumed.png')
+
+
+def test_checkpoint_refuses_another_render(tmp_path):
+    part = _smoke_renderer(2)
+    part.render()
+    ck = str(tmp_path / 'ck.npz')
+    part.save_checkpoint(ck)
+    other = _smoke_renderer(4)
+    other.max_depth = 7  # render-time attribute: checked when the render resumes
+    other.load_checkpoint(ck)
+    with pytest.raises(ValueError, match='max_depth'):
+        other.render(resume=True)
+    with pytest.raises(ValueError, match='load_checkpoint'):
+        _smoke_renderer(4).render(resume=True)
+
+
+def test_periodic_checkpoints_during_render(tmp_path):
+    r = _smoke_renderer(6)
+    r.checkpoint_path = str(tmp_path / 'auto.npz')
+    r.render()
+    with np.load(r.checkpoint_path, allow_pickle=False) as z:
+        assert int(z['next_sample']) == 4  # the last chunk boundary before the end
