@@ -102,7 +102,7 @@ def test_interactive_viewer_headless(tmp_path):
     assert not np.array_equal(r3.accum.cpu().numpy(), r.accum.cpu().numpy())
 
 
-def _smoke_renderer(spp, out='/dev/null'):
+def _smoke_renderer(spp, out):
     from ptmi import scenes
     from ptmi.renderer import TaichiRenderer
     random.seed(1234)
@@ -120,10 +120,10 @@ def test_checkpoint_resume_is_bit_identical(tmp_path):
     saved, loaded into a new renderer and resumed equals the uninterrupted
     6-sample render bit for bit (samples keyed by (seed, pixel, sample),
     accumulated in sample order)."""
-    full = _smoke_renderer(6)
+    full = _smoke_renderer(6, str(tmp_path / 'full.png'))
     full.render()
     ref = full.accum.cpu().numpy()
-    part = _smoke_renderer(4)
+    part = _smoke_renderer(4, str(tmp_path / 'part.png'))
     part.render()
     ck = str(tmp_path / 'ck.npz')
     part.save_checkpoint(ck)
@@ -137,21 +137,21 @@ def test_checkpoint_resume_is_bit_identical(tmp_path):
 
 
 def test_checkpoint_refuses_another_render(tmp_path):
-    part = _smoke_renderer(2)
+    part = _smoke_renderer(2, str(tmp_path / 'part.png'))
     part.render()
     ck = str(tmp_path / 'ck.npz')
     part.save_checkpoint(ck)
-    other = _smoke_renderer(4)
+    other = _smoke_renderer(4, str(tmp_path / 'other.png'))
     other.max_depth = 7  # render-time attribute: checked when the render resumes
     other.load_checkpoint(ck)
     with pytest.raises(ValueError, match='max_depth'):
         other.render(resume=True)
     with pytest.raises(ValueError, match='load_checkpoint'):
-        _smoke_renderer(4).render(resume=True)
+        _smoke_renderer(4, str(tmp_path / 'none.png')).render(resume=True)
 
 
 def test_periodic_checkpoints_during_render(tmp_path):
-    r = _smoke_renderer(6)
+    r = _smoke_renderer(6, str(tmp_path / 'auto.png'))
     r.checkpoint_path = str(tmp_path / 'auto.npz')
     r.render()
     with np.load(r.checkpoint_path, allow_pickle=False) as z:
