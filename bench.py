@@ -92,6 +92,9 @@ def parse():
     p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
                    help='nccl = RCCL over xGMI (the product path); gloo only to rehearse the multi-rank flow '
                         'with several ranks on one GPU (host-side reduce)')
+    p.add_argument('--no-overlap', action='store_true',
+                   help='megakernel: each step waits for the previous one to finish (default: consecutive '
+                        'steps overlap, Integrator.render_mk_overlapped)')
     p.add_argument('--traversal', choices=('stack', 'stackless'), default='stack',
                    help="BVH traversal: the reference's default stack walk (traverse_bvh_legacy, kernels.py:625) "
                         'or its USE_STACKLESS_TRAVERSAL walk (traverse_bvh_stackless, kernels.py:453)')
@@ -217,7 +220,11 @@ def main():
     shard = Shard(rank, world, a.shard)
     frame = device.make_frame(cam, bg, a.max_depth, a.seed, W, H, band=shard.band(), traversal=a.traversal)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
-    render = integ.render_mk if a.variant == 'mk' else integ.render_wf
+    if a.variant == 'mk':
+        def render(fr, acc_, s0, n):
+            integ.render_mk(fr, acc_, s0, n, overlap=not a.no_overlap)
+    else:
+        render = integ.render_wf
     sps = a.spp_per_step
 
     def sample_base(step):

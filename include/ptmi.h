@@ -154,11 +154,28 @@ int ptmi_mk_render(const ptmi_scene_view *scene, const ptmi_frame *frame, float 
  * workspace: device memory (16-byte aligned)
  * of at least ptmi_mk_workspace_bytes(frame, 1) bytes;
  * ptmi_mk_workspace_bytes(frame, B) = 12 * pixels * B (rounded up to 256) +
- * 256 lets one batch hold B samples. Asynchronous, graph-capturable. */
+ * 2048 (8 work-counter lines) lets one batch hold B samples. Asynchronous, graph-capturable. */
 size_t ptmi_mk_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_mk_render_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                       size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
                       uint64_t *counters, void *stream);
+
+/* The two halves of ptmi_mk_render_ws for one batch, for callers that
+ * schedule them on different streams: ptmi_mk_trace_ws runs the megakernel
+ * for samples [sample_begin, sample_begin + sample_count) of every pixel of
+ * the frame into the workspace's staging slots (the accumulator is not
+ * touched; the whole call must fit one batch: workspace_bytes >=
+ * ptmi_mk_workspace_bytes(frame, sample_count)); ptmi_mk_resolve_ws then
+ * adds those sample_count staged colours into accum in sample order. Trace
+ * then resolve gives, bit for bit, what ptmi_mk_render_ws gives. With two
+ * workspaces a caller can start the next batch's trace while the previous
+ * one drains (its last long paths leave most of the chip idle; ~1.5 ms per
+ * launch on vol2_final_scene) and keep the resolves in order on one stream. */
+int ptmi_mk_trace_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
+                     size_t workspace_bytes, int32_t sample_begin, int32_t sample_count, uint64_t *counters,
+                     void *stream);
+int ptmi_mk_resolve_ws(const ptmi_frame *frame, const void *workspace, size_t workspace_bytes, float *accum,
+                       int32_t sample_count, void *stream);
 
 /* Wavefront: replaces generate_camera_rays / intersect_rays /
  * shade_miss_rays / reset_next_ray_count / shade_and_scatter /

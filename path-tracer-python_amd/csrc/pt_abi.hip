@@ -232,6 +232,44 @@ int ptmi_mk_render_ws(const ptmi_scene_view* scene, const ptmi_frame* frame, voi
                    "mk_render_ws");
 }
 
+int ptmi_mk_trace_ws(const ptmi_scene_view* scene, const ptmi_frame* frame, void* workspace, size_t workspace_bytes,
+                     int32_t sample_begin, int32_t sample_count, uint64_t* counters, void* stream) {
+  DevScene sc;
+  DevFrame fr;
+  int rc = to_dev_scene(scene, sc);
+  if (rc) return rc;
+  if ((rc = to_dev_frame(frame, fr))) return rc;
+  if ((rc = check_traversal(sc, fr))) return rc;
+  if (sample_begin < 0 || sample_count < 1) return fail(PTMI_EINVAL, "bad sample range");
+  const int32_t npix = fr.w * fr.n_rows;
+  if (npix == 0) return PTMI_OK;
+  if ((int64_t)sample_count > mk_max_batch(fr))
+    return fail(PTMI_ECAPACITY, "%d samples exceed one batch's 2^32 item ids", sample_count);
+  const size_t need = mk_workspace_bytes(npix, sample_count);
+  if (!workspace || !aligned16(workspace) || workspace_bytes < need)
+    return fail(PTMI_EINVAL, "workspace too small/misaligned for one batch (%zu < %zu)", workspace_bytes, need);
+  return check_hip(mk_trace_staged(sc, fr, stack_needed(scene), workspace, sample_begin, sample_count,
+                                   (unsigned long long*)counters, (hipStream_t)stream),
+                   "mk_trace_ws");
+}
+
+int ptmi_mk_resolve_ws(const ptmi_frame* frame, const void* workspace, size_t workspace_bytes, float* accum,
+                       int32_t sample_count, void* stream) {
+  DevFrame fr;
+  int rc = to_dev_frame(frame, fr);
+  if (rc) return rc;
+  if (!accum) return fail(PTMI_EINVAL, "accum is NULL");
+  if (sample_count < 1) return fail(PTMI_EINVAL, "sample_count must be >= 1");
+  const int32_t npix = fr.w * fr.n_rows;
+  if (npix == 0) return PTMI_OK;
+  const size_t need = mk_workspace_bytes(npix, sample_count);
+  if (!workspace || !aligned16(workspace) || workspace_bytes < need)
+    return fail(PTMI_EINVAL, "workspace too small/misaligned for one batch (%zu < %zu)", workspace_bytes, need);
+  return check_hip(launch_stage_resolve(fr, (const float*)workspace, npix, sample_count, accum, kProfMkResolve,
+                                        (hipStream_t)stream),
+                   "mk_resolve_ws");
+}
+
 size_t ptmi_wf_workspace_bytes(const ptmi_frame* frame, int32_t batch_samples) {
   DevFrame fr;
   if (to_dev_frame(frame, fr)) return 0;

@@ -19,6 +19,12 @@ size_t mk_workspace_bytes(int32_t npix, int32_t batch);
 hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
                             size_t ws_bytes, float* accum, int32_t s_begin, int32_t s_count,
                             unsigned long long* counters, hipStream_t stream);
+// The two halves of one staged batch, for callers that schedule them
+// themselves (ptmi_mk_trace_ws / ptmi_mk_resolve_ws): the megakernel into the
+// workspace's staging, and the in-order resolve into accum.
+hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
+                           int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream);
+int64_t mk_max_batch(const DevFrame& fr);
 hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws, size_t ws_bytes,
                      float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
                      hipStream_t stream);

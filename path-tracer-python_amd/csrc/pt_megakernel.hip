@@ -126,12 +126,35 @@ static inline FastDiv fast_div(uint32_t d) {
 }
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (uint32_t)(((uint64_t)n * f.m) >> f.sh); }
 
+// Unit counters: the units are split into PTMI_MK_SHARDS contiguous shards,
+// each with its own counter on its own 256-B line, and wave w pulls from shard
+// w % PTMI_MK_SHARDS first (one shard per XCD under round-robin placement),
+// then steals from the others. One device-scope counter saturates near 88
+// returning atomics per us (MI355X_MICROARCH.md, "dequeue"), and a launch
+// makes ~10^5 fetches, most of them small ones in its tail, where every wave
+// is waiting for its next unit.
+#ifndef PTMI_MK_SHARDS
+#define PTMI_MK_SHARDS 8
+#endif
+// Shard s holds tiles s, s + S, s + 2S, ... (interleaved across the image, so
+// every shard costs about the same; 0: contiguous unit ranges, whose shards
+// drain at different times). A/B on MI355X, C2, 64-spp calls (overlapped):
+// one counter 2448 (2479), 8 contiguous shards 2320 (2546), 8 interleaved
+// 2560 (2597), 4 interleaved 2552 (2590) Msamples/s; 16-spp calls 1954 ->
+// 2324 (profiles/r02/ab/ab_mk_shards.log).
+#ifndef PTMI_MK_SHARD_INTERLEAVE
+#define PTMI_MK_SHARD_INTERLEAVE 1
+#endif
+constexpr int kMkShards = PTMI_MK_SHARDS;
+constexpr int kMkCtlLine = 64;  // int32 words per 256-B counter line
+
 struct MkWork {
-  int32_t* ctl;      // next unit (zeroed before the launch)
+  int32_t* ctl;      // kMkShards counters, one per 256-B line: units taken from each shard (zeroed before the launch)
+  int32_t shard_len; // units per shard (the last one may be short)
   int32_t csamp;     // most units per fetch
   int32_t tiles_x;   // 8x8 tiles per row
   int32_t nb;        // samples of the batch (units per tile)
-  FastDiv by_nb, by_tiles_x;
+  FastDiv by_nb, by_tiles_x, by_len;
   int32_t nunits;    // units of the batch (multiple of csamp)
   int32_t tail_div;  // TAIL_DIV * waves of the grid
 };
@@ -200,9 +223,17 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
   };
   auto locate = [&](uint32_t k) -> Loc {
     if (kPersist) {
+#if PTMI_MK_SHARD_INTERLEAVE
+      // shard-contiguous unit numbering: shard s holds tiles s, s + S, s + 2S, ...
+      const uint32_t v = k >> 6, sh = fdiv(v, wk.by_len), j = v - sh * (uint32_t)wk.shard_len;
+      const uint32_t tq = fdiv(j, wk.by_nb), t = tq * (uint32_t)kMkShards + sh, ty = fdiv(t, wk.by_tiles_x);
+      return Loc{fr.x0 + (int32_t)(t - ty * (uint32_t)wk.tiles_x) * 8, (int32_t)ty * 8,
+                 s_begin + (int32_t)(j - tq * (uint32_t)wk.nb)};
+#else
       const uint32_t u = k >> 6, t = fdiv(u, wk.by_nb), ty = fdiv(t, wk.by_tiles_x);
       return Loc{fr.x0 + (int32_t)(t - ty * (uint32_t)wk.tiles_x) * 8, (int32_t)ty * 8,
                  s_begin + (int32_t)(u - t * (uint32_t)wk.nb)};
+#endif
     }
     return Loc{sq_x, sq_y, s0 + (int32_t)(k >> 6)};
   };
@@ -430,12 +461,21 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) vo
         if (n > avail && !drained) {  // one fetch covers it: a unit is 64 items
           int32_t u0 = 0;
           if (lane == 0) {
-            const int32_t cur = __hip_atomic_load(wk.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int32_t take = max(1, min(wk.csamp, (wk.nunits - cur) / wk.tail_div));
-            u0 = cur < wk.nunits ? atomicAdd(wk.ctl, take) : wk.nunits;
-            const int32_t u1 = min(u0 + take, wk.nunits);
-            u0 = u0 < wk.nunits ? u0 : -1;
-            if (u0 >= 0) wend = 64u * (uint32_t)u1;  // lane 0's copy, broadcast below
+            u0 = -1;
+            for (int a = 0; a < kMkShards; ++a) {  // home shard first, then steal
+              const int32_t sh = (int32_t)((blockIdx.x + (unsigned)a) % (unsigned)kMkShards);
+              const int32_t lo = sh * wk.shard_len, hi = min(lo + wk.shard_len, wk.nunits);
+              int32_t* c = wk.ctl + sh * kMkCtlLine;
+              const int32_t cur = lo + __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (cur >= hi) continue;
+              const int32_t take = max(1, min(wk.csamp, (hi - cur) / wk.tail_div));
+              const int32_t t = lo + atomicAdd(c, take);
+              if (t < hi) {
+                u0 = t;
+                wend = 64u * (uint32_t)min(t + take, hi);  // lane 0's copy, broadcast below
+                break;
+              }
+            }
           }
           u0 = __shfl(u0, 0);
           wend = __shfl(wend, 0);
@@ -586,14 +626,18 @@ static size_t mk_staging_bytes(int32_t npix, int32_t batch) {
   return (3 * sizeof(float) * (size_t)npix * (size_t)batch + 255) & ~(size_t)255;
 }
 
-size_t mk_workspace_bytes(int32_t npix, int32_t batch) {  // staging + one 256-B counter line
+size_t mk_workspace_bytes(int32_t npix, int32_t batch) {  // staging + the shards' 256-B counter lines
   if (npix <= 0 || batch <= 0) return 0;
-  return mk_staging_bytes(npix, batch) + 256;
+  return mk_staging_bytes(npix, batch) + 256 * kMkShards;
 }
 
+// The megakernel of one staged batch: every (sample, pixel) colour of the
+// batch into staging[sample][pixel]; the accumulator is not touched (the
+// resolve is launch_stage_resolve, on the caller's schedule).
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float* staging, float* accum,
-                                   int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream) {
+static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float* staging, int32_t s_begin,
+                                  int32_t nb, unsigned long long* counters, hipStream_t stream) {
+  float* accum = nullptr;  // staged kernels write staging only
   const unsigned tx = (unsigned)((fr.w + kMkTile - 1) / kMkTile), ty = (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile);
   const int64_t tiles = (int64_t)tx * ty;
 #if PTMI_MK_PERSIST
@@ -610,7 +654,18 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   wk.tiles_x = (int32_t)tx;
   wk.nb = nb;
   if (tiles * nb * 64 >= (1ll << 32)) return hipErrorInvalidValue;  // item ids are 32-bit
+#if PTMI_MK_SHARD_INTERLEAVE
+  // shard s: tiles s, s + S, ... (interleaved across the image, so every shard
+  // costs about the same); virtual units past the last tile decode to rows
+  // outside the frame and are skipped
+  wk.shard_len = (int32_t)((tiles + kMkShards - 1) / kMkShards) * nb;
+  wk.nunits = wk.shard_len * kMkShards;
+  if ((int64_t)wk.nunits * 64 >= (1ll << 32)) return hipErrorInvalidValue;
+#else
   wk.nunits = (int32_t)(tiles * nb);
+  wk.shard_len = (wk.nunits + kMkShards - 1) / kMkShards;
+#endif
+  wk.by_len = fast_div((uint32_t)wk.shard_len);
   wk.by_nb = fast_div((uint32_t)nb);
   wk.by_tiles_x = fast_div((uint32_t)wk.tiles_x);
 #ifdef PTMI_MK_PERSIST_WPC
@@ -619,8 +674,9 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
   int64_t waves = (int64_t)(per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
   const int64_t chunks = wk.nunits;
   if (waves > chunks) waves = chunks;
-  wk.tail_div = (int32_t)(PTMI_MK_TAIL_DIV * waves);
-  (void)hipMemsetAsync(wk.ctl, 0, sizeof(int32_t), stream);
+  const int64_t tdiv = PTMI_MK_TAIL_DIV * waves / kMkShards;  // per shard: the waves pulling from it
+  wk.tail_div = (int32_t)(tdiv > 1 ? tdiv : 1);
+  (void)hipMemsetAsync(wk.ctl, 0, 256 * kMkShards, stream);
   prof_begin(kProfMk, stream);
   hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, nb, staging, counters, wk);
@@ -636,9 +692,26 @@ static hipError_t launch_mk_staged(const DevScene& sc, const DevFrame& fr, float
                      sc, fr, accum, s_begin, nb, chunk, staging, counters, MkWork{});
   prof_end(kProfMk, stream);
 #endif
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return launch_stage_resolve(fr, staging, fr.w * fr.n_rows, nb, accum, kProfMkResolve, stream);
+  return hipGetLastError();
+}
+
+hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
+                           int32_t s_begin, int32_t nb, unsigned long long* counters, hipStream_t stream) {
+  float* st = (float*)ws;
+  if (fr.traversal == PTMI_TRAV_STACKLESS)
+    return launch_mk_trace<1, PTMI_TRAV_STACKLESS>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) return launch_mk_trace<16>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed <= 20) return launch_mk_trace<20>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed <= 24) return launch_mk_trace<24>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed <= 32) return launch_mk_trace<32>(sc, fr, st, s_begin, nb, counters, stream);
+  return launch_mk_trace<64>(sc, fr, st, s_begin, nb, counters, stream);
+}
+
+int64_t mk_max_batch(const DevFrame& fr) {
+  // item ids (tile, sample, pixel of the 8x8 tile) are 32-bit: tiles * batch * 64 < 2^32
+  const int64_t tiles = (int64_t)((fr.w + kMkTile - 1) / kMkTile) * ((fr.n_rows + kMkTile - 1) / kMkTile);
+  const int64_t padded = (tiles + kMkShards - 1) / kMkShards * kMkShards;  // interleaved shards' virtual units
+  return tiles > 0 ? ((1ll << 32) - 1) / (padded * 64) : 0;
 }
 
 hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
@@ -649,23 +722,15 @@ hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stac
     return mk_render(sc, fr, stack_needed, accum, s_begin, s_count, counters, stream);
   const int32_t npix = fr.w * fr.n_rows;
   int32_t batch = s_count;
-  // item ids (tile, sample, pixel of the 8x8 tile) are 32-bit: tiles * batch * 64 < 2^32
-  const int64_t max_batch = ((1ll << 32) - 1) / (tiles * 64);
+  const int64_t max_batch = mk_max_batch(fr);
   if (max_batch < 1) return hipErrorInvalidValue;
   if (batch > max_batch) batch = (int32_t)max_batch;
   while (batch > 1 && mk_workspace_bytes(npix, batch) > ws_bytes) batch = (batch + 1) / 2;
   if (mk_workspace_bytes(npix, batch) > ws_bytes) return hipErrorInvalidValue;
   for (int32_t b0 = 0; b0 < s_count; b0 += batch) {
     const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
-    float* st = (float*)ws;
-    hipError_t e;
-    if (fr.traversal == PTMI_TRAV_STACKLESS)
-      e = launch_mk_staged<1, PTMI_TRAV_STACKLESS>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
-    else if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) e = launch_mk_staged<16>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
-    else if (stack_needed <= 20) e = launch_mk_staged<20>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
-    else if (stack_needed <= 24) e = launch_mk_staged<24>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
-    else if (stack_needed <= 32) e = launch_mk_staged<32>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
-    else e = launch_mk_staged<64>(sc, fr, st, accum, s_begin + b0, nb, counters, stream);
+    hipError_t e = mk_trace_staged(sc, fr, stack_needed, ws, s_begin + b0, nb, counters, stream);
+    if (e == hipSuccess) e = launch_stage_resolve(fr, (const float*)ws, npix, nb, accum, kProfMkResolve, stream);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -54,7 +54,7 @@ TRAVERSALS = {'stack': 0, 'stackless': 1}
 
 
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',
-           'ptmi_mk_render_ws', 'ptmi_wf_workspace_bytes',
+           'ptmi_mk_render_ws', 'ptmi_mk_trace_ws', 'ptmi_mk_resolve_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
            'ptmi_prof_stop', 'ptmi_node_bytes')
 PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve', 'mk_resolve')
@@ -96,6 +96,9 @@ def load(path: str = LIB_PATH):
     lib.ptmi_mk_workspace_bytes.restype = C.c_size_t
     lib.ptmi_mk_render_ws.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,
                                       C.c_int32, P, P]
+    lib.ptmi_mk_trace_ws.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, C.c_int32, C.c_int32,
+                                     P, P]
+    lib.ptmi_mk_resolve_ws.argtypes = [C.POINTER(Frame), P, C.c_size_t, P, C.c_int32, P]
     lib.ptmi_wf_workspace_bytes.argtypes = [C.POINTER(Frame), C.c_int32]
     lib.ptmi_wf_workspace_bytes.restype = C.c_size_t
     lib.ptmi_wf_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,

@@ -162,8 +162,13 @@ class Integrator:
     # staged colours (ptmi_mk_render_ws); single samples accumulate directly
     MK_STAGED_MIN_SAMPLES = 2
 
-    def render_mk(self, frame, accum, sample_begin, sample_count, stream=None, staged=None):
+    def render_mk(self, frame, accum, sample_begin, sample_count, stream=None, staged=None, overlap=False):
+        """Megakernel render of samples [sample_begin, sample_begin + sample_count)
+        added into accum in sample order. overlap=True: consecutive calls
+        pipeline (see render_mk_overlapped)."""
         _check_accum(accum, frame, self.scene.device)
+        if overlap:
+            return self.render_mk_overlapped(frame, accum, sample_begin, sample_count, stream)
         if staged is None:
             staged = int(sample_count) >= self.MK_STAGED_MIN_SAMPLES
         with self._dev():
@@ -182,6 +187,64 @@ class Integrator:
 
     # staging budget for the per-(sample, pixel) colour slots of one batch
     STAGING_BYTES = 1 << 30
+
+    def render_mk_overlapped(self, frame, accum, sample_begin, sample_count, stream=None):
+        """Megakernel calls whose launches overlap: each batch is traced
+        (ptmi_mk_trace_ws) on one of two side streams into one of two
+        workspaces, alternately, and resolved (ptmi_mk_resolve_ws) on the
+        caller's stream in call order, so the next call's megakernel fills
+        the chip while the previous one's last long paths drain (~1.5 ms of a
+        17-ms vol2 launch otherwise leaves most of the chip idle). Results
+        are bit-identical to render_mk: the resolves add the same staged
+        colours in the same sample order.
+
+        Ordering: a trace waits for the caller's stream as it was when the
+        *previous* overlapped call was made (that covers the resolve two
+        calls back, the last reader of its workspace) — not for later work,
+        which may include the previous trace's resolve. So the scene must not
+        change between overlapped calls, and work on the caller's stream
+        after this call sees the resolved accumulator as usual."""
+        import torch
+        dev = self.scene.device
+        caller = stream if stream is not None else torch.cuda.current_stream(dev)
+        npix = frame.w * len(frame_pixel_rows(frame))
+        if npix == 0 or sample_count <= 0:
+            return
+        per = max(1, min(int(sample_count), self.STAGING_BYTES // max(1, 12 * npix)))
+        with self._dev():
+            if getattr(self, '_ov', None) is None:
+                self._ov = {'streams': [torch.cuda.Stream(dev), torch.cuda.Stream(dev)], 'ws': [None, None],
+                            'k': 0, 'prev_entry': None}
+            ov = self._ov
+            b = 0
+            while b < sample_count:
+                n = min(per, int(sample_count) - b)
+                h = ov['k'] % 2
+                ov['k'] += 1
+                need = int(self.lib.ptmi_mk_workspace_bytes(C.byref(frame), n))
+                if need == 0:
+                    _lib.check(-1, 'ptmi_mk_workspace_bytes')
+                ws = ov['ws'][h]
+                if ws is None or ws.numel() * 4 < need:
+                    torch.cuda.synchronize(dev)  # the old half may still be read by a trace or a resolve
+                    ws = torch.empty((need + 15) // 16 * 4, dtype=torch.float32, device=dev)
+                    ov['ws'][h] = ws
+                entry = torch.cuda.Event()
+                entry.record(caller)
+                side = ov['streams'][h]
+                side.wait_event(ov['prev_entry'] if ov['prev_entry'] is not None else entry)
+                ov['prev_entry'] = entry
+                _lib.check(self.lib.ptmi_mk_trace_ws(C.byref(self.scene.view), C.byref(frame),
+                                                     C.c_void_p(ws.data_ptr()), ws.numel() * 4,
+                                                     int(sample_begin) + b, n, self._cnt(),
+                                                     C.c_void_p(side.cuda_stream)), 'ptmi_mk_trace_ws')
+                traced = torch.cuda.Event()
+                traced.record(side)
+                caller.wait_event(traced)
+                _lib.check(self.lib.ptmi_mk_resolve_ws(C.byref(frame), C.c_void_p(ws.data_ptr()), ws.numel() * 4,
+                                                       C.c_void_p(accum.data_ptr()), n,
+                                                       C.c_void_p(caller.cuda_stream)), 'ptmi_mk_resolve_ws')
+                b += n
 
     def workspace(self, frame, sample_count=1, kind='wf'):
         """Cached device workspace (torch) big enough for one batch of the call

@@ -104,3 +104,28 @@ def test_staged_megakernel_equals_direct(band):
         torch.cuda.synchronize()
         out.append(acc.cpu().numpy())
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize('traversal', ['stack', 'stackless'])
+def test_overlapped_megakernel_is_bit_identical(traversal):
+    """render_mk(overlap=True): traces on two side streams into two workspaces,
+    resolves in call order on the caller's stream (ptmi_mk_trace_ws /
+    ptmi_mk_resolve_ws) == the plain staged calls, bit for bit, counters too."""
+    import torch
+    from ptmi import device
+    from parity_helpers import scene_inputs
+    sa, cam, bg = scene_inputs('vol2_final_scene', 800)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, 800, 800, (96, 200, 200, 136), traversal=traversal)
+    out, cnt = [], []
+    for overlap in (False, True):
+        acc = torch.zeros((800, 800, 3), dtype=torch.float32, device='cuda')
+        acc[:] = 0.25
+        integ.reset_counters()
+        for s0, n in ((0, 5), (5, 1), (6, 7), (13, 3), (16, 2)):
+            integ.render_mk(fr, acc, s0, n, overlap=overlap)
+        torch.cuda.synchronize()
+        out.append(acc.cpu().numpy())
+        cnt.append(integ.read_counters())
+    assert np.array_equal(out[0], out[1])
+    assert cnt[0] == cnt[1]

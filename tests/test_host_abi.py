@@ -117,8 +117,8 @@ def test_render_rejects_bad_arguments_before_touching_device():
     assert rc == _lib.PTMI_EINVAL and 'workspace' in lib.ptmi_last_error().decode()
     rc = lib.ptmi_mk_render_ws(C.byref(v), C.byref(f), C.c_void_p(256), 1 << 20, None, 0, 2, None, None)
     assert rc == _lib.PTMI_EINVAL and 'accum' in lib.ptmi_last_error().decode()
-    assert lib.ptmi_mk_workspace_bytes(C.byref(f), 1) == 16 * 8 * 12 + (-(16 * 8 * 12) % 256) + 256  # + work counter line
-    assert lib.ptmi_mk_workspace_bytes(C.byref(f), 10) == 16 * 8 * 12 * 10 + 256
+    assert lib.ptmi_mk_workspace_bytes(C.byref(f), 1) == 16 * 8 * 12 + (-(16 * 8 * 12) % 256) + 2048  # + 8 counter lines
+    assert lib.ptmi_mk_workspace_bytes(C.byref(f), 10) == 16 * 8 * 12 * 10 + 2048
     assert lib.ptmi_mk_workspace_bytes(C.byref(f), 0) == 0
 
 
