@@ -87,6 +87,14 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
+#ifndef PTMI_MK_MIN_WAVES_16
+// 16-slot kernels (leaf depth <= 15, e.g. vol2): 16 * 8 B * 64 lanes * 20
+// waves fill the 160 KiB LDS, and without SLP vectorization (Makefile) the
+// kernel fits 96 VGPRs with no spills, so 5 waves/SIMD (A/B on MI355X,
+// parity-identical: C2 +0.5 % over the 4-wave 20-slot kernel;
+// profiles/r02/ab/ab_no_slp.log). With SLP on it spilled 148 B/lane: -20 %.
+#define PTMI_MK_MIN_WAVES_16 5
+#endif
 
 // Block = PTMI_MK_BLOCK_WAVES waves: 4 -> a 16x16 pixel tile, 1 -> 8x8.
 #ifndef PTMI_MK_BLOCK_WAVES
@@ -163,10 +171,11 @@ static_assert(PTMI_MK_BLOCK_WAVES == 4 || PTMI_MK_BLOCK_WAVES == 1, "block = 1 o
 
 template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
-// (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the 4-wave VGPR budget of 128.
+// (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the VGPR budget of that many
+// waves (96 at 5, 128 at 4).
 // TRAV = PTMI_TRAV_STACKLESS (STACK 1: no stack) walks the reference's
 // stackless traversal instead (TravSL, pt_device.hpp).
-__global__ __launch_bounds__(kMkBlock, (STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
+__global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
   constexpr bool kPersist = STAGED && PTMI_MK_PERSIST;
@@ -612,7 +621,7 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
 
 // ---------------------------------------------------------------- staged
 #ifndef PTMI_MK_STAGED_MIN_STACK
-#define PTMI_MK_STAGED_MIN_STACK 0  // staged: STACK 16 scenes use the 20-slot kernel (the 16-slot one spills 12 B/lane; same 4 waves/SIMD): +0.8 % C2
+#define PTMI_MK_STAGED_MIN_STACK 16  // staged: STACK 16 scenes use the 16-slot kernel at 5 waves/SIMD (PTMI_MK_MIN_WAVES_16)
 #endif
 #ifndef PTMI_MK_TARGET_BLOCKS
 #define PTMI_MK_TARGET_BLOCKS (16384 * 4 / PTMI_MK_BLOCK_WAVES)  // ~16 rounds of the chip's wave slots
