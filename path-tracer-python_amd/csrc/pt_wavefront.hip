@@ -514,7 +514,10 @@ __device__ __forceinline__ void sorted_writeback(const Queue& q, int32_t i, bool
 
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
 // medium-boundary hits go to their shard's medium queue segment.
-__global__ __launch_bounds__(kWfBlock) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
+#ifndef PTMI_WF_SHADE_MIN_WAVES
+#define PTMI_WF_SHADE_MIN_WAVES 5  // 96 VGPRs, no spills: A/B C3 +0.8 %; 6 waves (48 B spills) -2.7 % (profiles/r02/ab/ab_wf_occupancy.log)
+#endif
+__global__ __launch_bounds__(kWfBlock, PTMI_WF_SHADE_MIN_WAVES) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
                                                    unsigned long long* __restrict__ counters) {
   const Queue q = wb.q;
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
