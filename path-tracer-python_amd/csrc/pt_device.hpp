@@ -341,7 +341,26 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // (profiles/r01/ab_leaf_top.log). Kept: packed pairs, precomputed centres,
 // branch-free pushes.
 
+#ifndef PTMI_TRAV_SCALAR
+// The node step's child pairs as two scalar f32 ops (1) or one v_pk_*_f32
+// (0). A packed f32 op costs a wave about the issue time of the two scalar
+// ops it replaces (MI355X_MICROARCH.md constants, 'vector-instruction ISSUE
+// cost' and the packed-f32 filler row), and the pairs need operand shuffles.
+// A/B on MI355X, parity-identical, after -fno-slp-vectorize: C2 +5.5 %,
+// C3 and C4 within noise (profiles/r02/ab/ab_trav_scalar.log). Round 1
+// measured the packed form +2-3 % with SLP packing the scalar form itself.
+#define PTMI_TRAV_SCALAR 1
+#endif
+#if PTMI_TRAV_SCALAR
+struct pt_f2 {
+  float x, y;
+};
+__device__ __forceinline__ pt_f2 operator+(pt_f2 a, pt_f2 b) { return pt_f2{a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ pt_f2 operator-(pt_f2 a, pt_f2 b) { return pt_f2{a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ pt_f2 operator*(pt_f2 a, pt_f2 b) { return pt_f2{a.x * b.x, a.y * b.y}; }
+#else
 typedef float pt_f2 __attribute__((ext_vector_type(2)));
+#endif
 
 struct Stack {
   uint2* slot0;  // &lds[tid]; slot k at slot0[k * SB] (SB = threads per block)
