@@ -184,4 +184,25 @@ PT_HD float pt_acosf(float x) {
  * ((x*x)*(x*x))*x. */
 PT_HD float pt_pow5f(float x) { float x2 = x * x; return (x2 * x2) * x; }
 
+/* Correctly rounded x / a through a reciprocal of a shared by many quotients
+ * (the HIP sphere test divides both roots by the per-ray a = dot(d, d)); the
+ * oracle itself always writes x / a. pt_recip_for_div(a) is RN(1/a), or NaN
+ * when a is outside [2^-50, 2^50]. In pt_div_by, q = RN(x * ra) is within one
+ * ulp of x/a, the remainder x - a*q is exact in one fma, and RN(q + rem * ra)
+ * is RN(x/a) (Markstein's theorem) unless something under- or overflows.
+ * With a and q in [2^-50, 2^50] nothing does: the remainder is a multiple of
+ * 2^(e_a + e_q - 46) >= 2^-146 of at most 24 significant bits, so it is
+ * exactly representable. Any other quotient (and NaN) takes the plain
+ * division. tests/test_contract.py checks pt_div_by == x / a bit for bit. */
+PT_HD float pt_recip_for_div(float a) {
+    return (a >= 0x1p-50f && a <= 0x1p50f) ? 1.0f / a : __builtin_nanf("");
+}
+PT_HD float pt_div_by(float x, float a, float ra) {
+    const float q = x * ra;
+    float r = fmaf(fmaf(-a, q, x), ra, q);
+    const float aq = fabsf(q);
+    if (__builtin_expect(!(aq >= 0x1p-50f && aq <= 0x1p50f), 0)) r = x / a;
+    return r;
+}
+
 #endif /* PTMI_MATH_H */

@@ -170,7 +170,7 @@ def traverse(oscene, o, d, tmin=0.001, tmax=1e10, traversal='stack'):
     return bool(hit), float(t[0]), int(ty[0]), int(ix[0])
 
 
-MATH_FNS = {'sin': 0, 'cos': 1, 'log': 2, 'acos': 3, 'atan2': 4, 'pow5': 5}
+MATH_FNS = {'sin': 0, 'cos': 1, 'log': 2, 'acos': 3, 'atan2': 4, 'pow5': 5, 'div_by': 6}
 
 
 def math_probe(fn, x, y=None):

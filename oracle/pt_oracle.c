@@ -665,6 +665,7 @@ void or_math_probe(int fn, const float *x, const float *y, float *out, int n) {
         case 3: out[i] = pt_acosf(x[i]); break;
         case 4: out[i] = pt_atan2f(x[i], y[i]); break;
         case 5: out[i] = pt_pow5f(x[i]); break;
+        case 6: out[i] = pt_div_by(x[i], y[i], pt_recip_for_div(y[i])); break;  /* test of the HIP-side helper */
         default: out[i] = 0.0f;
         }
     }

@@ -168,11 +168,23 @@ __device__ __forceinline__ bool pt_all2(bool a, bool b) {
 // normal are recomputed at shading time from (o, d, t) with the same
 // operation order the reference uses inside the hit functions.
 
+#ifndef PTMI_SPHERE_MARKSTEIN
+// Sphere roots (h -+ sqrt(disc)) / a through a per-ray reciprocal of a
+// (pt_div_by, include/ptmi_math.h): A/B on MI355X, parity-identical: C2 +0.9 %, C5 +0.6 %, C3
+// +0.3 % (profiles/r02/ab/ab_sphere_markstein.log)
+#define PTMI_SPHERE_MARKSTEIN 1
+#endif
 __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, float tmin, float tmax,
                                              float& t) {  // kernels.py:209-248
   pt_v3 c = pt_v3f(s.x, s.y, s.z);
   pt_v3 oc = pt_sub(c, o);
   float a = pt_dot(d, d);
+#if PTMI_SPHERE_MARKSTEIN
+  const float ra = pt_recip_for_div(a);  // loop-invariant in a traversal: hoisted per segment
+#define PT_SPH_DIV(x) pt_div_by((x), a, ra)
+#else
+#define PT_SPH_DIV(x) ((x) / a)
+#endif
   float h = pt_dot(d, oc);
   float cc = pt_dot(oc, oc) - s.w * s.w;
   float disc = h * h - a * cc;
@@ -187,11 +199,12 @@ __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, f
 #endif
   if (disc >= 0.0f) {
     float sq = sqrtf(disc);
-    float root = (h - sq) / a;
-    if (root < tmin || root > tmax) root = (h + sq) / a;
+    float root = PT_SPH_DIV(h - sq);
+    if (root < tmin || root > tmax) root = PT_SPH_DIV(h + sq);
     if (pt_all2(root >= tmin, root <= tmax)) { t = root; return true; }
   }
   return false;
+#undef PT_SPH_DIV
 }
 
 __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const float4 c, const float4 e, pt_v3 o,

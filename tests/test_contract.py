@@ -109,3 +109,44 @@ def test_rng_statistics():
     # first draws of neighbouring pixels / samples are not correlated
     firsts = np.array([oracle.rng_probe(0, p, 0, 1)[0][0] for p in range(4000)])
     assert abs(np.corrcoef(firsts[:-1], firsts[1:])[0, 1]) < 0.05
+
+
+def _div_cases(rng, n):
+    """(x, a) pairs for the shared-reciprocal division: log-uniform magnitudes
+    over and past the guard range, the megakernel's a = |d|^2 ~ 1 regime, and
+    the IEEE special values."""
+    def logu(lo, hi, k):
+        return (2.0 ** rng.uniform(lo, hi, k)) * rng.choice([-1.0, 1.0], k)
+    xs = [logu(-70, 70, n), logu(-30, 30, n), logu(-10, 14, n)]
+    as_ = [np.abs(logu(-60, 60, n)), np.abs(logu(-8, 8, n)),
+           (1.0 + rng.integers(-64, 64, n) * 2.0 ** -23)]  # a within 64 ulp of 1
+    x = np.concatenate(xs).astype(np.float32)
+    a = np.concatenate(as_).astype(np.float32)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1.1754942e-38, 3.4028235e38,
+                   2.0 ** -50, 2.0 ** 50, 2.0 ** -50 * 0.99999994, 2.0 ** 50 * 1.0000001, 1.0, 3.0],
+                  np.float32)
+    gx, ga = np.meshgrid(sp, np.abs(sp))
+    return np.concatenate([x, gx.ravel(), sp]), np.concatenate([a, ga.ravel(), -np.abs(sp)])
+
+
+def test_shared_reciprocal_division_is_exact(rng):
+    """pt_div_by (include/ptmi_math.h; the HIP sphere test's division of both
+    roots by the per-ray a) equals the IEEE quotient x / a bit for bit."""
+    x, a = _div_cases(rng, 1_000_000)
+    got = oracle.math_probe('div_by', x, a)
+    with np.errstate(all='ignore'):
+        ref = x / a
+    nan = np.isnan(ref)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got[~nan].view(np.uint32), ref[~nan].view(np.uint32))
+
+
+def test_shared_reciprocal_division_near_midpoints(rng):
+    """Quotients close to a rounding midpoint: x = RN(a * m) for m with a
+    25th significant bit set, so x / a lies near a tie of m's neighbours."""
+    n = 500_000
+    m = (rng.integers(2 ** 24, 2 ** 25, n) | 1).astype(np.float64) * 2.0 ** rng.integers(-60, -10, n)
+    a = (2.0 ** rng.uniform(-20, 20, n)).astype(np.float32)
+    x = (m * a.astype(np.float64)).astype(np.float32)
+    got = oracle.math_probe('div_by', x, a)
+    assert np.array_equal(got.view(np.uint32), (x / a).view(np.uint32))
