@@ -23,7 +23,10 @@ Rank 0 at N=1 also times the CPU oracle (oracle/, a C restatement of the
 reference's kernels.py: the reference's ti.cpu path cannot run here, Taichi is
 absent) on a bounded slice of the same workload, and reports the dominant
 kernel's roofline from HIP events recorded around its launches in the timed
-region. `roofline.traffic` (PMC HBM-side bytes per launch, profiles/traffic.json)
+region: per-launch time = the union of the launches' [start, end] intervals
+divided by the launch count, because consecutive megakernel calls are
+pipelined on two streams and overlap (tools/trace_busy.py computes the same
+figure from a rocprofv3 kernel trace). `roofline.traffic` (PMC HBM-side bytes per launch, profiles/traffic.json)
 and `valu_diagnostic` (VALU issue share, lane efficiency and wave wait share of
 the dominant kernel, profiles/valu.json) come from committed rocprofv3 passes
 over the same workload (tools/pmc_traffic.py, tools/pmc_valu.py).
@@ -276,7 +279,10 @@ def main():
     value = samples_all / elapsed / 1e6
 
     prof = kt.result
-    dom = max((k for k in prof if prof[k]['launches']), key=lambda k: prof[k]['ms'])
+    # per-launch GPU time = union of the kind's launch intervals / launches
+    # (ptmi_prof_stop_busy): pipelined megakernel calls overlap their
+    # neighbours, so each launch's own start->end spans about two steps
+    dom = max((k for k in prof if prof[k]['launches']), key=lambda k: prof[k]['busy_ms'])
     S = cnt['segments'] / samples_rank
     M = cnt['medium'] / samples_rank
     b_sample = 44 + 24 + 128 * S  # SURVEY.md §8d whole-pipeline algorithmic bytes per sample
@@ -287,7 +293,7 @@ def main():
              'megakernel': samples_rank,
              'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
              'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]
-    dom_ms = prof[dom]['ms']
+    dom_ms = prof[dom]['busy_ms']
     launches = prof[dom]['launches']
     achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = measured_traffic(a, dom)
@@ -323,13 +329,17 @@ def main():
             'algorithmic_bytes_per_launch': round(units * unit_bytes / max(1, launches), 1),
             'unit_of_work': f'{unit_bytes:.1f} B per {unit_name[:-1] if unit_name.endswith("s") else unit_name}',
             'avg_launch_ms': round(dom_ms / max(1, launches), 5),
+            'avg_launch_own_ms': round(prof[dom]['ms'] / max(1, launches), 5),
             'launches': launches,
             'timing_truncated': bool(kt.truncated),
-            'timing': ('HIP events per launch on its stream, in the timed region' if inline else
-                       'HIP events per launch on its stream, in a second pass over the same steps'),
+            'timing': ('HIP events per launch on its stream, ' +
+                       ('in the timed region' if inline else 'in a second pass over the same steps') +
+                       "; avg_launch_ms = union of the launches' [start, end] intervals / launches "
+                       '(pipelined launches overlap; avg_launch_own_ms = mean start->end of one launch)'),
         },
         'valu_diagnostic': valu_diagnostic(a, dom),
         'kernels_ms': {k: round(v['ms'], 3) for k, v in prof.items() if v['launches']},
+        'kernels_busy_ms': {k: round(v['busy_ms'], 3) for k, v in prof.items() if v['launches']},
         'segments_per_sample': round(S, 4),
         'medium_traversals_per_sample': round(M, 4),
         'pipeline_algorithmic_GBps': round(value * 1e6 * b_sample / 1e9, 3),

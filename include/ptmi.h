@@ -232,6 +232,13 @@ int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int
 #define PTMI_PROF_KINDS 7
 int ptmi_prof_start(int32_t max_launches);
 int ptmi_prof_stop(double *ms_by_kernel, uint64_t *launches_by_kernel, int32_t n_kinds);
+/* As ptmi_prof_stop, plus per kind the busy time: the length of the union of
+ * its launches' [start, end] event intervals. Pipelined launches of one kind
+ * (two staged megakernel calls in flight on two streams, the wavefront's
+ * pipes) overlap, so their summed durations exceed the GPU time they take;
+ * busy / launches is the GPU time per launch. busy_ms_by_kernel may be NULL. */
+int ptmi_prof_stop_busy(double *ms_by_kernel, double *busy_ms_by_kernel, uint64_t *launches_by_kernel,
+                        int32_t n_kinds);
 
 #ifdef __cplusplus
 }

@@ -336,11 +336,17 @@ int ptmi_prof_start(int32_t max_launches) {
 }
 
 int ptmi_prof_stop(double* ms_by_kernel, uint64_t* launches_by_kernel, int32_t n_kinds) {
+  return ptmi_prof_stop_busy(ms_by_kernel, nullptr, launches_by_kernel, n_kinds);
+}
+
+int ptmi_prof_stop_busy(double* ms_by_kernel, double* busy_ms_by_kernel, uint64_t* launches_by_kernel,
+                        int32_t n_kinds) {
   if (!ms_by_kernel || !launches_by_kernel || n_kinds < 0) return fail(PTMI_EINVAL, "bad arguments");
-  int rc = prof_stop(ms_by_kernel, launches_by_kernel, n_kinds < kProfKinds ? n_kinds : kProfKinds);
+  int rc = prof_stop(ms_by_kernel, busy_ms_by_kernel, launches_by_kernel, n_kinds < kProfKinds ? n_kinds : kProfKinds);
   for (int32_t k = kProfKinds; k < n_kinds; ++k) {
     ms_by_kernel[k] = 0.0;
     launches_by_kernel[k] = 0;
+    if (busy_ms_by_kernel) busy_ms_by_kernel[k] = 0.0;
   }
   if (rc < 0) return fail(PTMI_EHIP, "event timing failed");
   if (rc > 0) return fail(PTMI_ECAPACITY, "more launches than the profiling pool; counts truncated");

@@ -5,6 +5,8 @@
 // the kernels' device durations; collection synchronises once at the end.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <utility>
 #include <vector>
 
 #include "pt_prof.hpp"
@@ -50,12 +52,19 @@ int prof_start(int32_t max_launches) {
   return 0;
 }
 
-int prof_stop(double* ms, uint64_t* launches, int32_t n_kinds) {
+// busy (may be null): per kind, the length of the union of its launches'
+// [start, end] intervals (event times relative to the session's first event).
+// Launches of one kind that overlap in time (the megakernel's pipelined calls
+// on two streams, the wavefront's pipes) count once there, so busy / launches
+// is the GPU time per launch, while ms sums each launch's own duration.
+int prof_stop(double* ms, double* busy, uint64_t* launches, int32_t n_kinds) {
   for (int32_t k = 0; k < n_kinds; ++k) {
     ms[k] = 0.0;
     launches[k] = 0;
+    if (busy) busy[k] = 0.0;
   }
   int rc = g_prof.overflow ? 1 : 0;
+  std::vector<std::vector<std::pair<double, double>>> iv((size_t)(n_kinds > 0 ? n_kinds : 0));
   for (size_t p = 0; p + 1 < g_prof.used; p += 2) {
     float t = 0.0f;
     // launches may sit on several streams (wavefront pipes): wait for each
@@ -65,6 +74,27 @@ int prof_stop(double* ms, uint64_t* launches, int32_t n_kinds) {
     if (k >= 0 && k < n_kinds) {
       ms[k] += (double)t;
       launches[k] += 1;
+      float t0 = 0.0f;
+      if (busy && hipEventElapsedTime(&t0, g_prof.ev[0], g_prof.ev[p]) == hipSuccess)
+        iv[(size_t)k].emplace_back((double)t0, (double)t0 + (double)t);
+    }
+  }
+  if (busy) {
+    for (int32_t k = 0; k < n_kinds; ++k) {
+      auto& v = iv[(size_t)k];
+      std::sort(v.begin(), v.end());
+      double cur_s = 0.0, cur_e = -1.0, sum = 0.0;
+      for (const auto& x : v) {
+        if (x.first > cur_e) {
+          if (cur_e > cur_s) sum += cur_e - cur_s;
+          cur_s = x.first;
+          cur_e = x.second;
+        } else if (x.second > cur_e) {
+          cur_e = x.second;
+        }
+      }
+      if (cur_e > cur_s) sum += cur_e - cur_s;
+      busy[k] = sum;
     }
   }
   for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);

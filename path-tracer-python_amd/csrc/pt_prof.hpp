@@ -9,5 +9,5 @@ enum : int32_t { kProfMk = 0, kProfWfGenerate = 1, kProfWfIntersect = 2, kProfWf
 void prof_begin(int32_t kind, hipStream_t s);
 void prof_end(int32_t kind, hipStream_t s);
 int prof_start(int32_t max_launches);
-int prof_stop(double* ms, uint64_t* launches, int32_t n_kinds);
+int prof_stop(double* ms, double* busy, uint64_t* launches, int32_t n_kinds);
 }  // namespace ptmi

@@ -56,7 +56,7 @@ TRAVERSALS = {'stack': 0, 'stackless': 1}
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',
            'ptmi_mk_render_ws', 'ptmi_mk_trace_ws', 'ptmi_mk_resolve_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
-           'ptmi_prof_stop', 'ptmi_node_bytes')
+           'ptmi_prof_stop', 'ptmi_prof_stop_busy', 'ptmi_node_bytes')
 PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve', 'mk_resolve')
 
 _lib = None
@@ -109,6 +109,7 @@ def load(path: str = LIB_PATH):
                                        C.POINTER(C.c_int32)]
     lib.ptmi_prof_start.argtypes = [C.c_int32]
     lib.ptmi_prof_stop.argtypes = [P, P, C.c_int32]
+    lib.ptmi_prof_stop_busy.argtypes = [P, P, P, C.c_int32]
     if lib.ptmi_version() != ABI_VERSION:
         raise PtmiError(f'libptmi ABI version {lib.ptmi_version()} != {ABI_VERSION} (rebuild libptmi.so)')
     _lib = lib
@@ -136,10 +137,14 @@ class KernelTimer:
     def __exit__(self, *exc):
         import numpy as np
         ms = np.zeros(len(PROF_KINDS), np.float64)
+        busy = np.zeros(len(PROF_KINDS), np.float64)
         n = np.zeros(len(PROF_KINDS), np.uint64)
-        rc = load().ptmi_prof_stop(C.c_void_p(ms.ctypes.data), C.c_void_p(n.ctypes.data), len(PROF_KINDS))
+        rc = load().ptmi_prof_stop_busy(C.c_void_p(ms.ctypes.data), C.c_void_p(busy.ctypes.data),
+                                        C.c_void_p(n.ctypes.data), len(PROF_KINDS))
         self.truncated = rc == PTMI_ECAPACITY  # more launches than events: totals cover the first ones
         if not self.truncated:
-            check(rc, 'ptmi_prof_stop')
-        self.result = {k: {'ms': float(ms[i]), 'launches': int(n[i])} for i, k in enumerate(PROF_KINDS)}
+            check(rc, 'ptmi_prof_stop_busy')
+        # ms: summed launch durations; busy_ms: union of the launches' intervals
+        self.result = {k: {'ms': float(ms[i]), 'busy_ms': float(busy[i]), 'launches': int(n[i])}
+                       for i, k in enumerate(PROF_KINDS)}
         return False
