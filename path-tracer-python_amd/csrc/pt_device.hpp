@@ -341,9 +341,9 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // Node layout (include/ptmi.h): the two children's box coordinates are
 // interleaved per component — {lo.x L,R | lo.y L,R}{lo.z L,R | hi.x L,R}
 // {hi.y L,R | hi.z L,R}{ref L, ref R, -, -} — so both children's slabs and
-// centre distances run as packed-f32 pairs (v_pk_add/v_pk_mul: one
-// instruction per component for both children). Packed ops are IEEE f32 per
-// half, so every value is bit-identical to the scalar restatement.
+// centre distances are computed as pairs (pt_f2): scalar f32 ops by default,
+// v_pk_add/v_pk_mul with PTMI_TRAV_SCALAR 0 (IEEE f32 per half either way, so
+// every value is bit-identical to the scalar restatement).
 //
 // A/B history on MI355X (all parity-identical): near-child shortcut with a
 // nested pop loop -17 %; top of stack in registers +0-2 % (mk) / -3 % (wf);
@@ -351,8 +351,9 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // culled pops in an inner loop -11 %; scalar-cache fetch of wave-uniform
 // nodes -1.7 % (the SGPR->VGPR moves cost more VALU than the texture path
 // saves); testing a leaf pushed on top in the expanding step itself -3 % mk
-// (profiles/r01/ab_leaf_top.log). Kept: packed pairs, precomputed centres,
-// branch-free pushes.
+// (profiles/r01/ab_leaf_top.log); near-child node prefetch across unrolled
+// pops -11 to -13 % (profiles/r02/ab/ab_trav_prefetch.log). Kept: child
+// pairs (scalar since round 2), precomputed centres, branch-free pushes.
 
 #ifndef PTMI_TRAV_SCALAR
 // The node step's child pairs as two scalar f32 ops (1) or one v_pk_*_f32
