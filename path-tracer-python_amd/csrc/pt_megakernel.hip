@@ -84,6 +84,13 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_NT
 #define PTMI_MK_NT 0
 #endif
+#ifndef PTMI_MK_ONE_BEGIN
+// One trav_begin call site per pass of the outer loop: lanes continuing a path
+// and lanes starting one (refill) mark need_seg and begin together after the
+// refill, instead of two divergent copies of trav_begin (3 divisions + the
+// root slab) in one shading round.
+#define PTMI_MK_ONE_BEGIN 1
+#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -280,6 +287,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
   tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
   bool hold = false;  // PTMI_MK_HOLD_NOISE: a traced Perlin-textured hit waiting for more of its kind
+  bool need_seg = false;  // PTMI_MK_ONE_BEGIN: begin a segment after this pass's refill
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
     trav_begin<STACK, kMkBlock>(sc, tr, st, ps.dir, ps.o, em ? ps.t_entry + 0.0001f : kTMin, kTMax);  // :418/:1057
@@ -452,11 +460,19 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
           live = s < s0 + ns;
           if (live) {
             start_path(fr, px, py, s, ps);
+#if PTMI_MK_ONE_BEGIN
+            need_seg = true;
+#else
             begin_segment();
+#endif
           }
         }
       } else {
+#if PTMI_MK_ONE_BEGIN
+        need_seg = true;  // next segment of this path (or its medium exit search)
+#else
         begin_segment();  // next segment of this path (or its medium exit search)
+#endif
       }
     }
     if (kPersist) {  // hand the wave's next items to the lanes without a path, fetching units as needed
@@ -504,10 +520,20 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
           if (bind(item)) {
             start_path(fr, px, py, s, ps);
             live = true;
+#if PTMI_MK_ONE_BEGIN
+            need_seg = true;
+#else
             begin_segment();
+#endif
           }
         }
       }
+#if PTMI_MK_ONE_BEGIN
+      if (need_seg) {
+        need_seg = false;
+        begin_segment();
+      }
+#endif
 #if PTMI_PROBE == 2
       {
         const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -526,13 +552,29 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
           if (item < total && bind(item)) {
             start_path(fr, px, py, s, ps);
             live = true;
+#if PTMI_MK_ONE_BEGIN
+            need_seg = true;
+#else
             begin_segment();
+#endif
           }
         }
         next += (uint32_t)__popcll(want);
       }
+#if PTMI_MK_ONE_BEGIN
+      if (need_seg) {
+        need_seg = false;
+        begin_segment();
+      }
+#endif
       if (__ballot(live) == 0ull && next >= total) break;
     } else {
+#if PTMI_MK_ONE_BEGIN
+      if (need_seg) {
+        need_seg = false;
+        begin_segment();
+      }
+#endif
       if (__ballot(live) == 0ull) break;
     }
   }
