@@ -1033,6 +1033,67 @@ __device__ __forceinline__ bool scatter(const DevScene& sc, int32_t ref, const M
   return false;  // emissive (3) and unknown types
 }
 
+// scatter() in two parts around its random unit vector (metal fuzz and
+// isotropic, kernels.py:865-871, 911-915), so that a kernel shading several
+// lanes can draw the unit vectors of every lane that needs one (these and the
+// constant-medium scatter, kernels.py:1082-1097) at one call site: the
+// rejection loop then runs once, to the wave's longest lane, instead of once
+// per divergent branch. Each lane's draws keep their order: nothing these
+// materials do before the unit vector draws, and the isotropic texture
+// (evaluated before it, at the Lambertian's texture site) draws nothing.
+// scatter_begin returns the pending kind; scatter_end finishes it.
+enum : int32_t { kRuvNone = 0, kRuvMetal = 1, kRuvIso = 2, kRuvMedium = 3 };
+
+__device__ __forceinline__ int32_t scatter_begin(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 dir,
+                                                 pt_v3 hp, pt_v3 n, Rng& r, pt_v3& sdir, pt_v3& att,
+                                                 bool& scattered) {
+  int32_t mt = m.mat_type();
+  sdir = pt_v3f(0.0f, 0.0f, 0.0f);
+  att = pt_v3f(1.0f, 1.0f, 1.0f);
+  scattered = false;
+  if (mt == 0 || mt == 4) att = eval_texture(sc, ref, m, hp);  // one texture site (draws nothing)
+  if (mt == 0) {
+    sdir = random_cosine_direction(n, r);
+    scattered = true;
+    return kRuvNone;
+  }
+  if (mt == 1) {
+    sdir = reflect3(pt_normalize(dir), n);  // the reflection; the fuzz is added in scatter_end
+    return kRuvMetal;
+  }
+  if (mt == 2) {
+    float ir = m.m1.w;
+    bool front = pt_dot(dir, n) < 0.0f;
+    pt_v3 nf = front ? n : pt_neg(n);
+    float ratio = front ? (1.0f / ir) : ir;
+    pt_v3 ud = pt_normalize(dir);
+    float ct = pt_minf(-pt_dot(ud, nf), 1.0f);
+    float st = sqrtf(1.0f - ct * ct);
+    bool cannot = ratio * st > 1.0f;
+    float u = r.next();  // unconditional draw
+    sdir = (cannot || reflectance(ct, ratio) > u) ? reflect3(ud, nf) : refract3(ud, nf, ratio);
+    scattered = true;
+    return kRuvNone;
+  }
+  if (mt == 4) return kRuvIso;
+  return kRuvNone;  // emissive (3) and unknown types
+}
+
+// v: the lane's random_unit_vector draw. Returns scattered.
+__device__ __forceinline__ bool scatter_end(const DevScene& sc, int32_t kind, int32_t ref, const Mat& m, pt_v3 hp,
+                                            pt_v3 n, pt_v3 v, pt_v3& sdir, pt_v3& att) {
+  if (kind == kRuvMetal) {
+    sdir = pt_add(sdir, pt_scale(v, m.m0.w));
+    if (pt_dot(sdir, n) > 0.0f) {
+      att = pt_v3f(m.m0.x, m.m0.y, m.m0.z);
+      return true;
+    }
+    return false;
+  }
+  sdir = v;  // kRuvIso (att: its texture, from scatter_begin)
+  return true;
+}
+
 __device__ __forceinline__ Mat load_mat(const DevScene& sc, int32_t g) {
   const float4* p = sc.mats + 5 * g;
   Mat m;

@@ -84,6 +84,19 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_NT
 #define PTMI_MK_NT 0
 #endif
+#ifndef PTMI_MK_ONE_RUV
+// One random_unit_vector call site per shading round (scatter_begin /
+// scatter_end, pt_device.hpp): metal, isotropic and constant-medium lanes draw
+// their unit vectors in one rejection loop. A/B on MI355X, parity-identical:
+// C2 -1.1 %, C4 +0.4 % (profiles/r02/ab/ab_one_scatter.log); off here, on in
+// the wavefront's wf_medium (PTMI_WF_ONE_SCATTER).
+#define PTMI_MK_ONE_RUV 0
+#endif
+#ifndef PTMI_MK_KEEP_SLOT
+// Staged mode: the path's staging slot is computed when its item is bound and
+// kept in a register, instead of decoding the item again when the path ends.
+#define PTMI_MK_KEEP_SLOT 1  // A/B: C2 +0.8 %, C4 +1 % (profiles/r02/ab/ab_one_scatter.log)
+#endif
 #ifndef PTMI_MK_ONE_BEGIN
 // One trav_begin call site per pass of the outer loop: lanes continuing a path
 // and lanes starting one (refill) mark need_seg and begin together after the
@@ -228,6 +241,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
   uint32_t wend = 0u;   // persistent: end of the wave's current units (items)
   bool drained = false; // persistent: the batch's units are all handed out
   int32_t px = 0, py = -1, lr = 0, s = s0;
+  uint32_t slot = 0u;  // PTMI_MK_KEEP_SLOT: staging slot of the bound item
   float* ap = nullptr;
   pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
   bool live = false;
@@ -260,6 +274,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
     px = l.x + (p & 7);
     lr = l.row + (p >> 3);
     py = (lr < fr.n_rows && px < fr.x0 + fr.w && s < s_begin + s_count) ? frame_row(fr, lr) : -1;
+#if PTMI_MK_KEEP_SLOT
+    if (STAGED) slot = (uint32_t)(s - s_begin) * (uint32_t)npix + (uint32_t)lr * (uint32_t)fr.w + (uint32_t)(px - fr.x0);
+#endif
     return py >= 0;
   };
   if (kPersist) {  // first units of the wave
@@ -361,6 +378,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
 
       bool done = false, scattered = false, passthrough = false, to_medium = false;
       pt_v3 hp, sdir, att;
+#if PTMI_MK_ONE_RUV
+      int32_t ruv = kRuvNone;
+#endif
       int32_t g = -1;
       if (!exit_mode) {
         if (!hit) {
@@ -390,7 +410,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
           // apply_constant_medium, kernels.py:421-448 (density m3.w)
           if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
             hp = mp;  // kernels.py:1082-1097
+#if PTMI_MK_ONE_RUV
+            ruv = kRuvMedium;
+#else
             sdir = random_unit_vector(ps.rng);
+#endif
             att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
             scattered = true;
           } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
@@ -404,12 +428,27 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
             st = ps.t_entry;
           }
         }
+#if PTMI_MK_ONE_RUV
+        pt_v3 n;
+        if (surface) {  // kernels.py:1120-1128
+          hp = pt_add(ps.o, pt_scale(ps.dir, st));
+          n = hit_normal(sc, sref, hp, ps.dir);
+          ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
+          ruv = scatter_begin(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att, scattered);
+        }
+        if (ruv != kRuvNone) {  // the round's one random_unit_vector site
+          const pt_v3 v = random_unit_vector(ps.rng);
+          if (ruv == kRuvMedium) sdir = v;
+          else scattered = scatter_end(sc, ruv, sref, m, hp, n, v, sdir, att);
+        }
+#else
         if (surface) {  // kernels.py:1120-1128
           hp = pt_add(ps.o, pt_scale(ps.dir, st));
           pt_v3 n = hit_normal(sc, sref, hp, ps.dir);
           ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
           scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
         }
+#endif
       }
 
       if (!done && !to_medium) {
@@ -437,12 +476,16 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STA
       if (done) {
         ++n_paths;
         if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
+#if PTMI_MK_KEEP_SLOT
+          float* o = staging + 3 * (size_t)slot;
+#else
           // slot of this lane's item (recomputed: pixel/sample need not stay live)
           const int32_t ip = (int32_t)(item & 63u);
           const Loc l = locate(item);
           const size_t srel = (size_t)(l.s - s_begin);
           float* o = staging + 3 * (srel * npix + (size_t)(l.row + (ip >> 3)) * (size_t)fr.w +
                                     (size_t)(l.x + (ip & 7) - fr.x0));
+#endif
 #if PTMI_MK_NT
           // A/B knob: non-temporal staging stores, +-0.3 % (profiles/r02/ab/ab_nontemporal.log)
           __builtin_nontemporal_store(ps.color.x, o);

@@ -424,6 +424,16 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
   return true;
 }
 
+#ifndef PTMI_WF_ONE_SCATTER
+// One scatter site and one random_unit_vector site per shading kernel
+// (scatter_begin / scatter_end, pt_device.hpp): wf_medium's deferred
+// Perlin-textured surfaces, boundary fallbacks and medium scatters share them,
+// so each divergent piece (material scatter, rejection loop) runs once per wave.
+// A/B on MI355X, parity-identical: C3 +0.8 %, mesh fog +0.6 %
+// (profiles/r02/ab/ab_one_scatter.log).
+#define PTMI_WF_ONE_SCATTER 1
+#endif
+
 // Per-lane tail of both shading kernels: keep a continuing ray in its slot,
 // or mark the slot of an ended path as waiting for work (the next
 // wf_intersect hands it the next item of its group's chunk).
@@ -444,7 +454,13 @@ __device__ __forceinline__ void shade_surface(const DevScene& sc, const DevFrame
   pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
   pt_v3 emit = emitted(m);
   pt_v3 sdir, att;
+#if PTMI_WF_ONE_SCATTER
+  bool sc_ok;
+  const int32_t ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, sc_ok);
+  if (ruv != kRuvNone) sc_ok = scatter_end(sc, ruv, ref, m, hp, nrm, random_unit_vector(r), sdir, att);
+#else
   bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
+#endif
   go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
   if (!go) {
     ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
@@ -602,6 +618,94 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
 #endif
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0;
+#if PTMI_WF_ONE_SCATTER
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
+    const int32_t j = base + (int32_t)threadIdx.x;
+    bool ended = false, go = false;
+    Ray cont;
+    int32_t i = -1, shard = 0;
+    const bool is_noise = PTMI_WF_DEFER_NOISE && j >= n && j < n + nn;
+    if (j < n) {  // medium-queue slot
+      int32_t off = j;
+#pragma unroll
+      for (int s = 0; s + 1 < kShards; ++s) {
+        if (shard == s && off >= cnt[s]) {
+          off -= cnt[s];
+          shard = s + 1;
+        }
+      }
+      i = s_load(wb.medq + shard * wb.medseg + off);
+    } else if (is_noise) {  // deferred surface slot (wf_shade), from the top of the segment
+      int32_t off = j - n;
+#pragma unroll
+      for (int s = 0; s + 1 < kShards; ++s) {
+        if (shard == s && off >= cntn[s]) {
+          off -= cntn[s];
+          shard = s + 1;
+        }
+      }
+      i = s_load(wb.medq + shard * wb.medseg + wb.medseg - 1 - off);
+    }
+    if (i >= 0) {
+      const float2 h = h_load(wb.hit + i);
+      const int32_t ref = __float_as_int(h.y);
+      const Ray ray = load_ray(wb.q, i);
+      float te = 0.0f;
+      int32_t rex = 0;
+      bool hx = false;
+      if (!is_noise)  // the exit search from t_entry + 1e-4 (kernels.py:417-419)
+        hx = traverse<STACK, kWfBlock, TRAV>(sc, ray.o, ray.d, h.x + 0.0001f, kTMax, st, te, rex);
+      const Mat m = load_mat(sc, mat_index(sc, ref));
+      Item it = decode_item(fr, wb, ray.item);
+      Rng r{path_key(fr, wb, it), ray.ctr};
+      bool surface = is_noise, scattered = false, passthrough = false;
+      int32_t ruv = kRuvNone;
+      pt_v3 hp, nrm, sdir, att, emit = pt_v3f(0.0f, 0.0f, 0.0f);
+      if (!is_noise) {
+        float t_exit;
+        pt_v3 mp;
+        if (medium_step(hx, te, h.x, m.m3.w, ray.o, ray.d, r, mp, t_exit)) {
+          hp = mp;
+          att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
+          ruv = kRuvMedium;
+          scattered = true;
+        } else if (t_exit > 0.0f) {  // passthrough: same depth, next wave (kernels.py:1342-1350)
+          passthrough = true;
+          int32_t wave = (int32_t)((ray.meta >> 8) & 0xffu);
+          if (wave + 1 < fr.max_depth) {
+            float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
+            cont = ray;
+            cont.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
+            cont.ctr = r.n;
+            cont.meta = ray.meta + (1u << 8);
+            go = true;
+          }
+        } else {  // fallback: the boundary as a surface (kernels.py:1352-1357)
+          surface = true;
+        }
+      }
+      if (surface) {  // one scatter site: deferred Perlin-textured hits and boundary fallbacks
+        hp = pt_add(ray.o, pt_scale(ray.d, h.x));
+        nrm = hit_normal(sc, ref, hp, ray.d);
+        emit = emitted(m);
+        ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, scattered);
+      }
+      if (ruv != kRuvNone) {  // one random_unit_vector site
+        const pt_v3 v = random_unit_vector(r);
+        if (ruv == kRuvMedium) sdir = v;
+        else scattered = scatter_end(sc, ruv, ref, m, hp, nrm, v, sdir, att);
+      }
+      if (!passthrough) go = scatter_epilogue(fr, scattered, hp, sdir, att, ray, r, cont);
+      if (!go) {
+        ended = true;  // emissive surfaces add their emission once (:1368-1375); other ends add 0
+        stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
+                                                                              : pt_v3f(0.0f, 0.0f, 0.0f));
+      }
+    }
+    finish_lane(wb, i, ended, go, cont);
+    n_ended += ended ? 1u : 0u;
+  }
+#else
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
@@ -676,6 +780,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
     finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
+#endif
   if (counters) block_flush(n_ended, lds_stack, counters + 2);
 }
 
