@@ -424,15 +424,12 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
   return true;
 }
 
-#ifndef PTMI_WF_ONE_SCATTER
 // One scatter site and one random_unit_vector site per shading kernel
 // (scatter_begin / scatter_end, pt_device.hpp): wf_medium's deferred
 // Perlin-textured surfaces, boundary fallbacks and medium scatters share them,
-// so each divergent piece (material scatter, rejection loop) runs once per wave.
-// A/B on MI355X, parity-identical: C3 +0.8 %, mesh fog +0.6 %
-// (profiles/r02/ab/ab_one_scatter.log).
-#define PTMI_WF_ONE_SCATTER 1
-#endif
+// so each divergent piece (material scatter, rejection loop) runs once per
+// wave. A/B on MI355X against separate sites, parity-identical: C3 +0.8 %,
+// mesh fog +0.6 % (profiles/r02/ab/ab_one_scatter.log).
 
 // Per-lane tail of both shading kernels: keep a continuing ray in its slot,
 // or mark the slot of an ended path as waiting for work (the next
@@ -454,13 +451,9 @@ __device__ __forceinline__ void shade_surface(const DevScene& sc, const DevFrame
   pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
   pt_v3 emit = emitted(m);
   pt_v3 sdir, att;
-#if PTMI_WF_ONE_SCATTER
-  bool sc_ok;
+  bool sc_ok;  // one unit-vector site for metal and isotropic lanes
   const int32_t ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, sc_ok);
   if (ruv != kRuvNone) sc_ok = scatter_end(sc, ruv, ref, m, hp, nrm, random_unit_vector(r), sdir, att);
-#else
-  bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
-#endif
   go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
   if (!go) {
     ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
@@ -618,7 +611,6 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
 #endif
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0;
-#if PTMI_WF_ONE_SCATTER
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
@@ -705,82 +697,6 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
     finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
-#else
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
-    const int32_t j = base + (int32_t)threadIdx.x;
-    bool ended = false, go = false;
-    Ray cont;
-    int32_t i = -1, shard = 0;
-#if PTMI_WF_DEFER_NOISE
-    if (j >= n && j < n + nn) {
-      int32_t off = j - n;
-#pragma unroll
-      for (int s = 0; s + 1 < kShards; ++s) {
-        if (shard == s && off >= cntn[s]) {
-          off -= cntn[s];
-          shard = s + 1;
-        }
-      }
-      i = s_load(wb.medq + shard * wb.medseg + wb.medseg - 1 - off);
-      const float2 h = h_load(wb.hit + i);
-      const int32_t ref = __float_as_int(h.y);
-      shade_surface(sc, fr, wb, load_ray(wb.q, i), h.x, ref, mat_index(sc, ref), ended, go, cont);
-    }
-#endif
-    if (j < n) {
-      int32_t off = j;
-#pragma unroll
-      for (int s = 0; s + 1 < kShards; ++s) {
-        if (shard == s && off >= cnt[s]) {
-          off -= cnt[s];
-          shard = s + 1;
-        }
-      }
-      i = s_load(wb.medq + shard * wb.medseg + off);
-      const float2 h = h_load(wb.hit + i);
-      const int32_t ref = __float_as_int(h.y);
-      const Ray ray = load_ray(wb.q, i);
-      const float t_entry = h.x;
-      float te;
-      int32_t rex;
-      const bool hx = traverse<STACK, kWfBlock, TRAV>(sc, ray.o, ray.d, t_entry + 0.0001f, kTMax, st, te, rex);
-      const Mat m = load_mat(sc, mat_index(sc, ref));
-      Item it = decode_item(fr, wb, ray.item);
-      Rng r{path_key(fr, wb, it), ray.ctr};
-      float t_exit;
-      pt_v3 mp;
-      pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
-      if (medium_step(hx, te, t_entry, m.m3.w, ray.o, ray.d, r, mp, t_exit)) {
-        pt_v3 sdir = random_unit_vector(r);
-        go = scatter_epilogue(fr, true, mp, sdir, pt_v3f(m.m4.x, m.m4.y, m.m4.z), ray, r, cont);
-      } else if (t_exit > 0.0f) {  // passthrough: same depth, next wave (kernels.py:1342-1350)
-        int32_t wave = (int32_t)((ray.meta >> 8) & 0xffu);
-        if (wave + 1 < fr.max_depth) {
-          float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
-          cont = ray;
-          cont.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
-          cont.ctr = r.n;
-          cont.meta = ray.meta + (1u << 8);
-          go = true;
-        }
-      } else {  // fallback (kernels.py:1352-1357)
-        pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, t_entry));
-        pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
-        emit = emitted(m);
-        pt_v3 sdir, att;
-        bool sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
-        go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
-      }
-      if (!go) {
-        ended = true;
-        stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
-                                                                              : pt_v3f(0.0f, 0.0f, 0.0f));
-      }
-    }
-    finish_lane(wb, i, ended, go, cont);
-    n_ended += ended ? 1u : 0u;
-  }
-#endif
   if (counters) block_flush(n_ended, lds_stack, counters + 2);
 }
 

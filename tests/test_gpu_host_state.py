@@ -8,7 +8,11 @@ the box's GPU):
 * the device a DeviceScene is bound to decides where its launches go, not
   whichever device happens to be current;
 * a staged megakernel call whose (tile, sample, pixel) item ids would pass
-  2^32 is split into batches instead of failing.
+  2^32 is split into batches instead of failing;
+* the profiler's busy time (ptmi_prof_stop_busy, bench.py's per-launch time
+  for the roofline) is the union of overlapping launches: pipelined
+  megakernel calls overlap, so it is below the summed durations and close to
+  the wall time of the calls.
 """
 import threading
 
@@ -121,3 +125,34 @@ def test_mk_staged_item_ids_past_2_to_32_split_into_batches():
     want = np.add.accumulate(np.full(n, np.float32(bg[0]), np.float32))[-1]
     assert acc[0, 0, 0].item() == want
     assert acc[0, 1:].abs().sum().item() == 0.0
+
+
+def test_prof_busy_time_is_the_union_of_overlapping_launches():
+    import time
+    import torch
+    from ptmi import device, _lib
+    sa, cam, _ = scene_inputs('vol2_final_scene', 800)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr, acc = _frame_acc(cam, (0, 0, cam['width'], cam['height']))
+    integ.render_mk(fr, acc, 0, 4, overlap=True)  # warm-up: workspaces, streams
+    torch.cuda.synchronize()
+    n, spp = 6, 8
+    with _lib.KernelTimer(max_launches=1000) as kt:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            integ.render_mk(fr, acc, 4 + k * spp, spp, overlap=True)
+        torch.cuda.synchronize()
+        wall_ms = (time.perf_counter() - t0) * 1e3
+    mk = kt.result['megakernel']
+    assert mk['launches'] == n and not kt.truncated
+    assert 0.0 < mk['busy_ms'] <= mk['ms'] + 1e-3   # a union never exceeds the sum
+    assert mk['busy_ms'] <= wall_ms * 1.02 + 0.1     # nor the wall time around the calls
+    assert mk['busy_ms'] >= 0.5 * wall_ms            # the megakernel is most of it
+    # non-overlapped launches: busy == summed durations (disjoint intervals)
+    with _lib.KernelTimer(max_launches=1000) as kt2:
+        for k in range(3):
+            integ.render_mk(fr, acc, 100 + k * spp, spp)
+            torch.cuda.synchronize()
+    mk2 = kt2.result['megakernel']
+    assert abs(mk2['busy_ms'] - mk2['ms']) <= 1e-3 * max(1.0, mk2['ms'])
