@@ -107,6 +107,14 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
+#ifndef PTMI_MK_EXACT_STACK
+// Staged kernels for leaf depth 16-18 (17-19 slots, e.g. C4's torus BVH) get
+// exactly the slots they need instead of the 20-slot kernel, and the 5-wave
+// VGPR budget: 17 slots leave LDS for 18 one-wave blocks per CU instead of 16.
+// A/B on MI355X, C4 (leaf depth 16), parity-identical: 1357 -> 1414 Msamples/s
+// (+4.2 %; profiles/r02/ab/ab_exact_stack.log).
+#define PTMI_MK_EXACT_STACK 1
+#endif
 #ifndef PTMI_MK_MIN_WAVES_16
 // 16-slot kernels (leaf depth <= 15, e.g. vol2): 16 * 8 B * 64 lanes * 20
 // waves fill the 160 KiB LDS, and without SLP vectorization (Makefile) the
@@ -195,7 +203,7 @@ template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves (96 at 5, 128 at 4).
 // TRAV = PTMI_TRAV_STACKLESS (STACK 1: no stack) walks the reference's
 // stackless traversal instead (TravSL, pt_device.hpp).
-__global__ __launch_bounds__(kMkBlock, (STACK <= 16 ? PTMI_MK_MIN_WAVES_16 : STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
+__global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && STACK < 20) ? PTMI_MK_MIN_WAVES_16 : STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
   constexpr bool kPersist = STAGED && PTMI_MK_PERSIST;
@@ -795,6 +803,11 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
   if (fr.traversal == PTMI_TRAV_STACKLESS)
     return launch_mk_trace<1, PTMI_TRAV_STACKLESS>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) return launch_mk_trace<16>(sc, fr, st, s_begin, nb, counters, stream);
+#if PTMI_MK_EXACT_STACK
+  if (stack_needed == 17) return launch_mk_trace<17>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed == 18) return launch_mk_trace<18>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed == 19) return launch_mk_trace<19>(sc, fr, st, s_begin, nb, counters, stream);
+#endif
   if (stack_needed <= 20) return launch_mk_trace<20>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= 24) return launch_mk_trace<24>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= 32) return launch_mk_trace<32>(sc, fr, st, s_begin, nb, counters, stream);

@@ -61,6 +61,11 @@ constexpr int kShards = 8;
 #define PTMI_WF_BLOCK 256  // threads per block of the queue kernels
 #endif
 constexpr int kWfBlock = PTMI_WF_BLOCK;
+#ifndef PTMI_WF_EXACT_STACK
+// Leaf depth 16-18 (17-19 slots): kernels with exactly the slots needed
+// instead of the 20-slot ones (more blocks per CU fit the LDS stacks).
+#define PTMI_WF_EXACT_STACK 0
+#endif
 constexpr uint32_t kDead = 0xffffffffu;     // item of a retired slot
 constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (assigned in wf_intersect)
 
@@ -957,6 +962,11 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     hipError_t e;
     if (fr.traversal == PTMI_TRAV_STACKLESS) e = wf_batch<1, PTMI_TRAV_STACKLESS>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+#if PTMI_WF_EXACT_STACK
+    else if (stack_needed == 17) e = wf_batch<17>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed == 18) e = wf_batch<18>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed == 19) e = wf_batch<19>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+#endif
     else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wbs, accum, nb, counters, stream, *ps);
