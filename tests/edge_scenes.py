@@ -4,9 +4,9 @@
 * ``single``: one sphere, so the BVH root is itself a leaf (root_ref < 0);
 * ``chain<N>``: N small spheres in a row under a hand-built *linear* BVH
   (every internal node has a leaf left child and an internal right child), so
-  the deepest leaf sits at depth N-1 and the integrator must dispatch its 24-,
-  32- or 64-slot traversal kernels, which the BASELINE scenes (leaf depth
-  <= 16) never reach. The flattened arrays follow the reference's layout
+  the deepest leaf sits at depth N-1 and the integrator must dispatch its 17-
+  to 20-slot (N = 17..20) or 24-, 32- or 64-slot traversal kernels, most of
+  which the BASELINE scenes (leaf depth <= 16) never reach. The flattened arrays follow the reference's layout
   (sah_bvh_builder.py:338-418 flatten: preorder, left child at i + 1, node
   box = union of the children's boxes, internal prim_type/prim_idx = -1).
 """

@@ -75,6 +75,17 @@ def test_deep_bvh_uses_wider_stacks(name, variant):
     _check(name, variant, 4)
 
 
+@pytest.mark.parametrize('name', ['chain17', 'chain18', 'chain19', 'chain20'])
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_leaf_depth_16_to_19_exact_slot_kernels(name, variant):
+    # leaf depth 16-18: the staged megakernel's 17-, 18- and 19-slot kernels
+    # (PTMI_MK_EXACT_STACK); 19: its 20-slot kernel; the wavefront's 20-slot ones
+    from ptmi import scene_data as sd
+    depth = sd.pack_device(edge_scene(name)[0]).max_leaf_depth
+    assert depth == int(name[5:]) - 1
+    _check(name, variant, 4)
+
+
 @pytest.mark.parametrize('max_depth', [1, 2])
 @pytest.mark.parametrize('variant', ['mk', 'wf'])
 def test_small_max_depth(variant, max_depth):
