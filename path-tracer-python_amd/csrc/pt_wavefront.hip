@@ -58,7 +58,8 @@ constexpr int kShards = 8;
 #define PTMI_WF_TAIL 2  // a shard hands out single units once it has < TAIL chunks per group left
 #endif
 #ifndef PTMI_WF_BLOCK
-#define PTMI_WF_BLOCK 256  // threads per block of the queue kernels
+#define PTMI_WF_BLOCK 128  // threads per block of the queue kernels (A/B on MI355X, parity-identical: 128 vs 256
+                           // C3 +1.2 %, mesh fog +1.7 %; 64: C3 -6 %, mesh fog +2.3 %; profiles/r02/ab/ab_wf_block.log)
 #endif
 constexpr int kWfBlock = PTMI_WF_BLOCK;
 #ifndef PTMI_WF_EXACT_STACK
