@@ -178,6 +178,12 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return 
 // one counter 2448 (2479), 8 contiguous shards 2320 (2546), 8 interleaved
 // 2560 (2597), 4 interleaved 2552 (2590) Msamples/s; 16-spp calls 1954 ->
 // 2324 (profiles/r02/ab/ab_mk_shards.log).
+#ifndef PTMI_MK_FETCH_ROLLED
+// The shard loop of a unit fetch kept rolled: unrolled, its 8 counter
+// addresses and bounds are hoisted out of the persistent loop into SGPRs,
+// which then spill to VGPR lanes (47 SGPR spills in the 16-slot kernel).
+#define PTMI_MK_FETCH_ROLLED 0
+#endif
 #ifndef PTMI_MK_SHARD_INTERLEAVE
 #define PTMI_MK_SHARD_INTERLEAVE 1
 #endif
@@ -538,6 +544,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           int32_t u0 = 0;
           if (lane == 0) {
             u0 = -1;
+#if PTMI_MK_FETCH_ROLLED
+#pragma unroll 1
+#endif
             for (int a = 0; a < kMkShards; ++a) {  // home shard first, then steal
               const int32_t sh = (int32_t)((blockIdx.x + (unsigned)a) % (unsigned)kMkShards);
               const int32_t lo = sh * wk.shard_len, hi = min(lo + wk.shard_len, wk.nunits);
