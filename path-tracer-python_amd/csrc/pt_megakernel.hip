@@ -63,6 +63,12 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
                              // with 3 pops per header pass 16 > 12)
 #endif
 
+#ifndef PTMI_MK_SHADE_AT_DEEP
+// The threshold for kernels with more than 16 stack slots (deep BVHs such as
+// C4's torus, whose traversals are longer and more uneven): A/B knob.
+#define PTMI_MK_SHADE_AT_DEEP PTMI_MK_SHADE_AT
+#endif
+
 #ifndef PTMI_MK_STEP_UNROLL
 #define PTMI_MK_STEP_UNROLL 3  // A/B with SHADE_AT 16: 3 pops per header pass +1.9 % C2, +2.6 % C4 (2: +1.5 %, 4: +1.6 %)
 #endif
@@ -343,7 +349,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy() && !hold) != 0ull) break;
+      if (nbusy <= (uint32_t)(STACK > 16 ? PTMI_MK_SHADE_AT_DEEP : PTMI_MK_SHADE_AT) && pt_ballot(trav && !tr.busy() && !hold) != 0ull) break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
