@@ -14,10 +14,15 @@ vol2_final_scene compiled arrays captured at random.seed(1234)
 (tests/golden/vol2_final_scene.npz), camera from the reference's camera math.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU; rank r renders its own disjoint shard of sample indices of the full
-image (weak scaling: per-GPU work fixed), then one RCCL reduce (sum) of the
-f32 accumulators to rank 0 inside the timed region. value = samples of all
-ranks / max-over-ranks wall time.
+per GPU. By default the image is tile-sharded (BASELINE.json
+configs[4]): rank r renders the interleaved row bands it owns for every sample
+of every step, so the total workload (W x H x spp_per_step x steps) is fixed
+and N GPUs split it (strong scaling); the bands' height is chosen so every
+rank owns the same number of rows. One RCCL reduce (sum) of the f32
+accumulators onto rank 0, inside the timed region, assembles the image, which
+is bit-identical to the 1-GPU render. value = total samples / max-over-ranks
+wall time. --shard samples keeps the weak-scaling alternative (every rank the
+whole image, disjoint sample indices).
 
 Rank 0 at N=1 also times the CPU oracle (oracle/, a C restatement of the
 reference's kernels.py: the reference's ti.cpu path cannot run here, Taichi is
@@ -51,7 +56,7 @@ PRESETS = {
     'c2': ('vol2_final_scene', 800, 'mk', 64, 16),       # configs[1]; 16 steps = the 1024-spp north star
     'c3': ('vol2_final_scene', 800, 'wf', 64, 16),       # configs[2]: wavefront, 1024 spp
     'c4': ('cornell_mesh_fog', 1024, 'mk', 32, 16),      # configs[3]: OBJ mesh + fog, 512 spp
-    'c5': ('vol2_final_scene_comparison', 3840, 'mk', 16, 32),  # configs[4]: 4K, 512 spp per GPU (4096 on 8)
+    'c5': ('vol2_final_scene_comparison', 3840, 'mk', 16, 256),  # configs[4]: 4K @ 4096 spp, tile-sharded
 }
 
 # Algorithmic HBM bytes per unit (DESIGN.md "Roofline"): what each kernel must
@@ -76,7 +81,7 @@ ALGO_BYTES = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
     p.add_argument('--preset', choices=sorted(PRESETS), default='c2',
@@ -101,9 +106,10 @@ def parse():
     p.add_argument('--traversal', choices=('stack', 'stackless'), default='stack',
                    help="BVH traversal: the reference's default stack walk (traverse_bvh_legacy, kernels.py:625) "
                         'or its USE_STACKLESS_TRAVERSAL walk (traverse_bvh_stackless, kernels.py:453)')
-    p.add_argument('--shard', choices=('samples', 'tiles'), default='samples',
-                   help='multi-GPU partition: disjoint sample shards (weak scaling) or row-band tiles (strong)')
-    a = p.parse_args()
+    p.add_argument('--shard', choices=('samples', 'tiles'), default='tiles',
+                   help='multi-GPU partition: row-band tiles of a fixed total workload (strong scaling, default; '
+                        'bit-identical to 1 GPU) or disjoint sample shards of the whole image (weak scaling)')
+    a = p.parse_args(argv)
     scene, width, variant, sps, steps = PRESETS[a.preset]
     a.scene = a.scene or scene
     a.width = a.width or width
@@ -196,12 +202,77 @@ def measured_traffic(a, kernel):
     return {'bytes_per_launch': r['bytes_per_launch'], 'source': r['source']}
 
 
+class BenchRun:
+    """The hot-path call shape of one bench rank: workload, device scene,
+    frame (this rank's bands), and one step = one render call of
+    spp_per_step samples. tests/test_gpu_bench_shapes.py drives this same
+    object to check the benchmarked calls against the oracle."""
+
+    def __init__(self, a, dev, rank=0, world=1):
+        from ptmi import device
+        from ptmi.distributed import Shard
+        self.a = a
+        self.sa, self.cam, self.bg, self.data_note = load_workload(a.scene, a.width)
+        self.W, self.H = self.cam['width'], self.cam['height']
+        self.integ = device.Integrator(device.DeviceScene(self.sa, dev))
+        self.shard = Shard.balanced(rank, world, a.shard, self.H)
+        self.frame = device.make_frame(self.cam, self.bg, a.max_depth, a.seed, self.W, self.H,
+                                       band=self.shard.band(), traversal=a.traversal)
+        self.sps = a.spp_per_step
+        self.rows = len(self.shard.rows(self.H))
+
+    def sample_base(self, step):
+        return self.shard.sample_range(step, self.sps)[0]
+
+    def render(self, acc, s0, n):
+        if self.a.variant == 'mk':
+            self.integ.render_mk(self.frame, acc, s0, n, overlap=not self.a.no_overlap)
+        else:
+            self.integ.render_wf(self.frame, acc, s0, n)
+
+    def step(self, acc, k):
+        """Step k: samples [sample_base(k), sample_base(k) + spp_per_step) of this rank's rows."""
+        self.render(acc, self.sample_base(k), self.sps)
+
+
+def describe(a, W, H, world, shard):
+    """Workload description of the JSON line: (total spp, scaling, config)."""
+    total_spp = a.spp_per_step * a.steps * (world if a.shard == 'samples' else 1)
+    rows_rank = len(shard.rows(H))
+    cfg = {
+        'workload': f'{a.scene} {W}x{H} @ {total_spp} spp in total ({a.steps} steps x {a.spp_per_step} spp'
+                    f'{" x " + str(world) + " sample shards" if a.shard == "samples" and world > 1 else ""}), '
+                    f'{"wavefront" if a.variant == "wf" else "megakernel"} integrator, max_depth {a.max_depth}',
+        'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'traversal': a.traversal,
+        'spp_per_step': a.spp_per_step, 'total_spp': total_spp,
+        'partition': a.shard,
+        'band_rows': shard.band()[0] if a.shard == 'tiles' and world > 1 else None,
+        'rows_per_rank': rows_rank,
+        'max_depth': a.max_depth, 'seed': a.seed,
+        'parallelism': (f'{a.shard}-shard x{world} + {"RCCL" if a.dist_backend == "nccl" else "gloo"} reduce'
+                        if world > 1 else 'single GPU'),
+    }
+    return total_spp, ('weak' if a.shard == 'samples' else 'strong'), cfg
+
+
+def gather_ranks(vals, dev, world):
+    """Per-rank float rows (all_gather) -> list of lists; [vals] for world 1."""
+    if world == 1:
+        return [list(vals)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
 def main():
     a = parse()
     import torch
     import torch.distributed as dist
-    from ptmi import device, scene_data as sd, _lib
-    from ptmi.distributed import Shard, max_over_ranks, reduce_accum
+    from ptmi import _lib
+    from ptmi.distributed import max_over_ranks, reduce_accum
 
     world = a.gpus
     rank = int(os.environ.get('RANK', '0'))
@@ -216,25 +287,19 @@ def main():
             dist.init_process_group('nccl', device_id=dev)
         else:
             dist.init_process_group('gloo')
+        if dist.get_world_size() != world:
+            sys.exit(f'--gpus {world} but torch.distributed has {dist.get_world_size()} ranks')
+    world_size = dist.get_world_size() if world > 1 else 1
 
-    sa, cam, bg, data_note = load_workload(a.scene, a.width)
-    W, H = cam['width'], cam['height']
-    integ = device.Integrator(device.DeviceScene(sa, dev))
-    shard = Shard(rank, world, a.shard)
-    frame = device.make_frame(cam, bg, a.max_depth, a.seed, W, H, band=shard.band(), traversal=a.traversal)
+    run = BenchRun(a, dev, rank, world)
+    integ, frame, sa, cam, bg = run.integ, run.frame, run.sa, run.cam, run.bg
+    W, H, sps = run.W, run.H, run.sps
+    data_note = run.data_note
+    shard = run.shard
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
-    if a.variant == 'mk':
-        def render(fr, acc_, s0, n):
-            integ.render_mk(fr, acc_, s0, n, overlap=not a.no_overlap)
-    else:
-        render = integ.render_wf
-    sps = a.spp_per_step
-
-    def sample_base(step):
-        return shard.sample_range(step, sps)[0]
 
     for k in range(a.warmup):
-        render(frame, acc, sample_base(k), sps)
+        run.step(acc, k)
     # warm the collective too: RCCL sets up a collective's channels on its
     # first call, which must not land in the timed region
     reduce_accum(acc, dst=0)
@@ -258,25 +323,31 @@ def main():
             dist.barrier()
         t0 = time.perf_counter()
         for k in range(a.steps):
-            render(frame, acc, sample_base(a.warmup + k), sps)
+            run.step(acc, a.warmup + k)
+        t_render_end = None
+        if world > 1:
+            torch.cuda.synchronize(dev)  # this rank's own render time (per-rank balance), then the reduce
+            t_render_end = time.perf_counter()
         reduce_accum(acc, dst=0)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
-        elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dev if a.dist_backend == 'nccl' else None)
+        elapsed_rank = time.perf_counter() - t0
+    render_rank = (t_render_end - t0) if t_render_end is not None else elapsed_rank
+    elapsed = max_over_ranks(elapsed_rank, dev if a.dist_backend == 'nccl' else None)
     cnt = integ.read_counters()
     if not inline:
         acc_k = torch.zeros_like(acc)
         with _lib.KernelTimer(max_launches=100_000) as kt:
             for k in range(a.steps):
-                render(frame, acc_k, sample_base(a.warmup + k), sps)
+                run.step(acc_k, a.warmup + k)
             torch.cuda.synchronize(dev)
         del acc_k
-    rows_rank = len(shard.rows(H))
+    rows_rank = run.rows
     samples_rank = W * rows_rank * sps * a.steps
     samples_all = samples_rank * world if a.shard == 'samples' else W * H * sps * a.steps
     value = samples_all / elapsed / 1e6
+    total_spp, scaling, config = describe(a, W, H, world, shard)
 
     prof = kt.result
     # per-launch GPU time = union of the kind's launch intervals / launches
@@ -295,40 +366,47 @@ def main():
              'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]
     dom_ms = prof[dom]['busy_ms']
     launches = prof[dom]['launches']
+    avg_launch_ms = dom_ms / max(1, launches)
     achieved = units * unit_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    traffic = measured_traffic(a, dom)
+    # the committed PMC passes were collected on the full frame at one GPU
+    traffic = measured_traffic(a, dom) if world == 1 or a.shard == 'samples' else None
+    valu = valu_diagnostic(a, dom)
+    per_rank = gather_ranks([rank, rows_rank, samples_rank, render_rank, elapsed_rank, dom_ms],
+                            dev if a.dist_backend == 'nccl' else 'cpu', world)
 
     out = {
         'metric': METRIC,
         'value': round(value, 3),
         'unit': 'Msamples/s',
         'n_gpus': world,
+        'world_size': world_size,
         'steps': a.steps,
         'warmup': a.warmup,
         'ms_per_step': round(elapsed * 1e3 / a.steps, 4),
         'higher_is_better': True,
-        'scaling': 'weak' if a.shard == 'samples' else 'strong',
+        'scaling': scaling,
         'vs_baseline': None,
         'dtype': 'f32',
         'data': data_note,
-        'config': {
-            'workload': f'{a.scene} {W}x{H}, {"wavefront" if a.variant == "wf" else "megakernel"} integrator, '
-                        f'{sps * a.steps} spp per GPU ({a.steps} steps x {sps} spp), max_depth {a.max_depth}',
-            'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant, 'traversal': a.traversal,
-            'spp_per_step': sps,
-            'spp_per_gpu': sps * a.steps if a.shard == 'samples' else f'{sps * a.steps} (rows 1/{world})', 'max_depth': a.max_depth, 'seed': a.seed,
-            'parallelism': (f'{a.shard}-shard x{world} + {"RCCL" if a.dist_backend == "nccl" else "gloo"} reduce'
-                            if world > 1 else 'single GPU'),
-        },
+        'config': config,
         'roofline': {
             'bound': 'hbm', 'kernel': dom,
             'achieved': round(achieved, 3), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBPS, 6),
             'traffic': traffic['bytes_per_launch'] if traffic else None,
             'traffic_source': traffic['source'] if traffic else None,
+            # what the counters say the kernel really moves to/from HBM (incl.
+            # Infinity-Cache hits): PMC bytes per launch / busy time per launch
+            'measured_GBps': round(traffic['bytes_per_launch'] / (avg_launch_ms * 1e-3) / 1e9, 3)
+            if traffic and avg_launch_ms > 0 else None,
+            # compute side of the same kernel: VALU issue share x lane efficiency
+            # (profiles/valu.json): the fraction of the chip's FP32 lanes doing work
+            'compute_frac': round(valu['valu_issue_frac'] * valu['lane_efficiency'], 4) if valu else None,
+            'achieved_note': ('achieved = algorithmic bytes (SURVEY.md §8d B_sample model) / busy time; '
+                              'it is not HBM traffic: see measured_GBps'),
             'algorithmic_bytes_per_launch': round(units * unit_bytes / max(1, launches), 1),
             'unit_of_work': f'{unit_bytes:.1f} B per {unit_name[:-1] if unit_name.endswith("s") else unit_name}',
-            'avg_launch_ms': round(dom_ms / max(1, launches), 5),
+            'avg_launch_ms': round(avg_launch_ms, 5),
             'avg_launch_own_ms': round(prof[dom]['ms'] / max(1, launches), 5),
             'launches': launches,
             'timing_truncated': bool(kt.truncated),
@@ -337,12 +415,14 @@ def main():
                        "; avg_launch_ms = union of the launches' [start, end] intervals / launches "
                        '(pipelined launches overlap; avg_launch_own_ms = mean start->end of one launch)'),
         },
-        'valu_diagnostic': valu_diagnostic(a, dom),
+        'valu_diagnostic': valu,
         'kernels_ms': {k: round(v['ms'], 3) for k, v in prof.items() if v['launches']},
         'kernels_busy_ms': {k: round(v['busy_ms'], 3) for k, v in prof.items() if v['launches']},
         'segments_per_sample': round(S, 4),
         'medium_traversals_per_sample': round(M, 4),
         'pipeline_algorithmic_GBps': round(value * 1e6 * b_sample / 1e9, 3),
+        'ranks': [{'rank': int(r[0]), 'rows': int(r[1]), 'samples': int(r[2]), 'render_s': round(r[3], 4),
+                   'elapsed_s': round(r[4], 4), 'kernel_busy_ms': round(r[5], 3)} for r in per_rank],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(sa, cam, bg, a.scene, a.variant, a.max_depth, a.seed, a.cpu_seconds)
@@ -352,7 +432,7 @@ def main():
         if a.save_image:
             from PIL import Image
             # tiles: every pixel has sps * steps samples; samples: each rank added its own
-            img = integ.tonemap(acc, sps * a.steps * (world if a.shard == "samples" else 1)).cpu().numpy()
+            img = integ.tonemap(acc, total_spp).cpu().numpy()
             Image.fromarray(img).save(a.save_image)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 5
+#define PTMI_ABI_VERSION 6
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -118,17 +118,19 @@ typedef struct ptmi_frame {
 
 /* Device counters (u64): [0] ray segments traced from the depth loop / waves,
  * [1] medium-exit traversals (kernels.py:417), [2] completed paths,
- * [3] reserved. Accumulated with atomics; pass NULL to skip. */
-#define PTMI_NUM_COUNTERS 4
+ * [3] paths ended by Russian roulette (kernels.py:1145-1157, the reference's
+ * rr_paths_killed, fields.py:295), [4] paths ended by the depth / wave budget
+ * (kernels.py:1139-1141, 1383; renderer.py:313: its max_depth_terminations,
+ * fields.py:287). Accumulated with atomics; pass NULL to skip. [3] and [4]
+ * since ABI v6 (the buffer must hold PTMI_NUM_COUNTERS entries). */
+#define PTMI_NUM_COUNTERS 5
 
 int ptmi_version(void);
 const char *ptmi_last_error(void);
 
 /* Byte stride of the library's BVH node array (the `nodes` layout above):
- * 80 for one child record per internal node, 256 for two-level packets
- * (record 0 = the node's children, records 1 and 2 = child 0's and child 1's
- * children, zero-filled when that child is a leaf; 16 B padding). Internal
- * refs are node index x this stride. */
+ * 80, one child record per internal node. Internal refs are node index x
+ * this stride. */
 int ptmi_node_bytes(void);
 
 /* Checks a scene view's counts, alignment and structural limits on the host. */
@@ -174,6 +176,10 @@ int ptmi_mk_render_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, voi
 int ptmi_mk_trace_ws(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                      size_t workspace_bytes, int32_t sample_begin, int32_t sample_count, uint64_t *counters,
                      void *stream);
+/* Largest sample_count one ptmi_mk_trace_ws batch of this frame accepts (its
+ * (8x8 tile, sample, pixel) item ids must stay below 2^32); 0 on a bad frame.
+ * ABI v6. */
+int64_t ptmi_mk_max_batch(const ptmi_frame *frame);
 int ptmi_mk_resolve_ws(const ptmi_frame *frame, const void *workspace, size_t workspace_bytes, float *accum,
                        int32_t sample_count, void *stream);
 

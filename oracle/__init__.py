@@ -44,7 +44,8 @@ class OrFrame(C.Structure):
 
 
 class OrStats(C.Structure):
-    _fields_ = [('segments', C.c_uint64), ('medium', C.c_uint64), ('paths', C.c_uint64)]
+    _fields_ = [('segments', C.c_uint64), ('medium', C.c_uint64), ('paths', C.c_uint64), ('rr', C.c_uint64),
+                ('depth_cap', C.c_uint64)]
 
 
 _lib = None
@@ -157,7 +158,8 @@ def render(oscene, frame, variant, accum, window, s_begin, s_count, threads=0):
                           x0, y0, w, h, s_begin, s_count, threads, C.byref(st))
     if rc != 0:
         raise RuntimeError(f'or_render failed: {rc}')
-    return {'segments': st.segments, 'medium': st.medium, 'paths': st.paths}
+    return {'segments': st.segments, 'medium': st.medium, 'paths': st.paths, 'rr': st.rr,
+            'depth_cap': st.depth_cap}
 
 
 def traverse(oscene, o, d, tmin=0.001, tmax=1e10, traversal='stack'):

@@ -521,13 +521,21 @@ static pt_v3 trace_ray_mk(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
                 o = hp;
                 d = sdir;
                 thr = pt_mul(thr, att);
-                if (depth + 1 >= fr->max_depth) break;
+                if (depth + 1 >= fr->max_depth) {
+                    if (st) st->depth_cap++;
+                    break;
+                }
                 if (depth + 1 >= 5) {
                     float sp = pt_minf(pt_maxf(pt_maxf(thr.x, thr.y), thr.z), 0.95f);
-                    if (draw(r) > sp) break;
+                    if (draw(r) > sp) {
+                        if (st) st->rr++;
+                        break;
+                    }
                     thr = pt_divs(thr, sp);
                 }
-            } else if (!passthrough) {
+            } else if (passthrough) {
+                if (depth + 1 >= fr->max_depth && st) st->depth_cap++;  /* the loop ends: kernels.py:1054 */
+            } else {
                 break;
             }
         } else {
@@ -575,6 +583,7 @@ static pt_v3 trace_ray_wf(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
             } else if (m.t_exit > 0.0f) {
                 float eps_t = 0.001f / sqrtf(pt_dot(d, d));
                 o = pt_add(o, pt_scale(d, m.t_exit + eps_t));
+                if (wave + 1 >= fr->max_depth && st) st->depth_cap++;  /* Q14 */
                 continue;                                     /* same depth, next wave */
             } else {
                 emit = emitted(sc, pt, pi);
@@ -591,13 +600,20 @@ static pt_v3 trace_ray_wf(const or_scene *sc, const or_frame *fr, pt_v3 ro, pt_v
         if (!scattered) break;
         pt_v3 nthr = pt_mul(thr, att);
         int ndepth = depth + 1;
-        if (ndepth >= fr->max_depth) break;
+        if (ndepth >= fr->max_depth) {
+            if (st) st->depth_cap++;
+            break;
+        }
         if (ndepth >= 5) {
             float sp = pt_minf(pt_maxf(pt_maxf(nthr.x, nthr.y), nthr.z), 0.95f);
-            if (draw(r) > sp) break;
+            if (draw(r) > sp) {
+                if (st) st->rr++;
+                break;
+            }
             nthr = pt_divs(nthr, sp);
         }
         o = hp; d = sdir; thr = nthr; depth = ndepth;
+        if (wave + 1 >= fr->max_depth && st) st->depth_cap++;  /* Q14: no wave left */
     }
     (void)have;
     return acc;
@@ -621,23 +637,26 @@ int or_render(const or_scene *sc, const or_frame *fr, int variant, float *accum,
         return -1;
     /* num_bvh_nodes == 0 (empty world, sah_bvh_builder.py:345-355) is legal: the root pop is
        skipped as an invalid node (kernels.py:660) and every path misses */
-    uint64_t seg = 0, med = 0, paths = 0;
+    uint64_t seg = 0, med = 0, paths = 0, rr = 0, cap = 0;
     long npix = (long)w * (long)h;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 8) reduction(+ : seg, med, paths)
+#pragma omp parallel for schedule(dynamic, 8) reduction(+ : seg, med, paths, rr, cap)
 #endif
     for (long q = 0; q < npix; ++q) {
         int px = x0 + (int)(q % w), py = y0 + (int)(q / w);
-        or_stats st = {0, 0, 0};
+        or_stats st = {0, 0, 0, 0, 0};
         float *a = accum + 3 * ((size_t)py * (size_t)fr->width + (size_t)px);
         for (int s = s_begin; s < s_begin + s_count; ++s) {
             pt_v3 c = trace_path(sc, fr, variant, px, py, s, &st);
             a[0] += c.x; a[1] += c.y; a[2] += c.z;          /* render_sample :1187 */
         }
-        seg += st.segments; med += st.medium; paths += st.paths;
+        seg += st.segments; med += st.medium; paths += st.paths; rr += st.rr; cap += st.depth_cap;
     }
-    if (stats) { stats->segments += seg; stats->medium += med; stats->paths += paths; }
+    if (stats) {
+        stats->segments += seg; stats->medium += med; stats->paths += paths;
+        stats->rr += rr; stats->depth_cap += cap;
+    }
     return 0;
 }
 

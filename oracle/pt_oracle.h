@@ -68,6 +68,8 @@ typedef struct or_stats {
     uint64_t segments;   /* traverse_bvh calls from the depth loop / waves */
     uint64_t medium;     /* medium-exit traversals (kernels.py:417) */
     uint64_t paths;
+    uint64_t rr;         /* paths ended by Russian roulette (kernels.py:1145-1157) */
+    uint64_t depth_cap;  /* paths ended by the depth / wave budget (kernels.py:1139-1141, 1383; renderer.py:313) */
 } or_stats;
 
 #ifdef __cplusplus

@@ -253,6 +253,12 @@ int ptmi_mk_trace_ws(const ptmi_scene_view* scene, const ptmi_frame* frame, void
                    "mk_trace_ws");
 }
 
+int64_t ptmi_mk_max_batch(const ptmi_frame* frame) {
+  DevFrame fr;
+  if (to_dev_frame(frame, fr)) return 0;
+  return mk_max_batch(fr);
+}
+
 int ptmi_mk_resolve_ws(const ptmi_frame* frame, const void* workspace, size_t workspace_bytes, float* accum,
                        int32_t sample_count, void* stream) {
   DevFrame fr;

@@ -20,6 +20,7 @@ constexpr float kTMin = 0.001f;     // kernels.py:1057, 1254
 constexpr float kTMax = 1e10f;
 constexpr int kRRMinDepth = 5;      // kernels.py:1050
 constexpr float kRRMaxProb = 0.95f; // kernels.py:1051
+constexpr int kNumCounters = PTMI_NUM_COUNTERS;  // include/ptmi.h
 constexpr int kBlock = 256;
 
 enum : int32_t { kSphere = 0, kTriangle = 1, kQuad = 2 };
@@ -132,71 +133,39 @@ __device__ __forceinline__ void get_ray(const DevFrame& fr, int32_t px, int32_t 
 }
 
 // ---------------------------------------------------------------- primitives
-#ifndef PTMI_LEAF_FLAT
-// leaf tests as one predicate instead of nested early-outs (bit 1 quad +
-// triangle, bit 2 sphere). A/B on MI355X, parity-identical: bit 1 -1 % mk,
-// -2 % wf; bit 2 within noise (profiles/r01/ab_leaf_flat.log)
-#define PTMI_LEAF_FLAT 0
-#endif
-#ifndef PTMI_LEAF_PRELOAD
-#define PTMI_LEAF_PRELOAD 1  // A/B on MI355X: +1.4 % C2, +4 % C4, +2.6 % wavefront
-#endif
-#ifndef PTMI_MASK_PRED
-#define PTMI_MASK_PRED 1
-#endif
+// Leaf primitives are loaded whole (one round trip) before their test (A/B on
+// MI355X: +1.4 % C2, +4 % C4, +2.6 % wavefront). A/B, not kept: the leaf tests
+// as one predicate instead of nested early-outs, -1 % mk, -2 % wf
+// (profiles/r01/ab_leaf_flat.log).
 // a && b && c && d of per-lane compares as lane masks (v_cmp into SGPR pairs,
 // s_and): the compiler otherwise materialises each compare with v_cndmask and
 // combines them with 16-bit VALU bit ops (~16 VALU per quad test on gfx950)
 __device__ __forceinline__ bool pt_all4(bool a, bool b, bool c, bool d) {
-#if PTMI_MASK_PRED
   return __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b) &
                                              __builtin_amdgcn_ballot_w64(c) & __builtin_amdgcn_ballot_w64(d));
-#else
-  return a && b && c && d;
-#endif
 }
 
 __device__ __forceinline__ bool pt_all2(bool a, bool b) {
-#if PTMI_MASK_PRED
   return __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b));
-#else
-  return a && b;
-#endif
 }
 
 // Each returns the candidate t (hit only if returned true); hit point and
 // normal are recomputed at shading time from (o, d, t) with the same
 // operation order the reference uses inside the hit functions.
 
-#ifndef PTMI_SPHERE_MARKSTEIN
 // Sphere roots (h -+ sqrt(disc)) / a through a per-ray reciprocal of a
 // (pt_div_by, include/ptmi_math.h): A/B on MI355X, parity-identical: C2 +0.9 %, C5 +0.6 %, C3
 // +0.3 % (profiles/r02/ab/ab_sphere_markstein.log)
-#define PTMI_SPHERE_MARKSTEIN 1
-#endif
 __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, float tmin, float tmax,
                                              float& t) {  // kernels.py:209-248
   pt_v3 c = pt_v3f(s.x, s.y, s.z);
   pt_v3 oc = pt_sub(c, o);
   float a = pt_dot(d, d);
-#if PTMI_SPHERE_MARKSTEIN
   const float ra = pt_recip_for_div(a);  // loop-invariant in a traversal: hoisted per segment
 #define PT_SPH_DIV(x) pt_div_by((x), a, ra)
-#else
-#define PT_SPH_DIV(x) ((x) / a)
-#endif
   float h = pt_dot(d, oc);
   float cc = pt_dot(oc, oc) - s.w * s.w;
   float disc = h * h - a * cc;
-#if PTMI_LEAF_FLAT & 2
-  {  // no early-out on disc < 0: its NaN roots fail every range test
-    const float sq = sqrtf(disc);
-    float root = (h - sq) / a;
-    if (root < tmin || root > tmax) root = (h + sq) / a;
-    t = root;
-    return (disc >= 0.0f) & (root >= tmin) & (root <= tmax);
-  }
-#endif
   if (disc >= 0.0f) {
     float sq = sqrtf(disc);
     float root = PT_SPH_DIV(h - sq);
@@ -211,19 +180,6 @@ __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const
                                            pt_v3 d, float tmin, float tmax, float& t) {  // kernels.py:311-362
   pt_v3 n = pt_v3f(a.x, a.y, a.z);
   float denom = pt_dot(n, d);
-#if PTMI_LEAF_FLAT & 1
-  {  // one predicate instead of nested early-outs (same values; a lane's t is used only on a hit)
-    const float tt = (a.w - pt_dot(n, o)) / denom;
-    const pt_v3 Q = pt_v3f(b.x, b.y, b.z), u = pt_v3f(b.w, c.x, c.y), v = pt_v3f(c.z, c.w, e.x);
-    const pt_v3 w = pt_v3f(e.y, e.z, e.w);
-    const pt_v3 pv = pt_sub(pt_add(o, pt_scale(d, tt)), Q);
-    const float alpha = pt_dot(w, pt_cross(pv, v));
-    const float beta = pt_dot(w, pt_cross(u, pv));
-    t = tt;
-    return (fabsf(denom) >= 1e-8f) & (tt >= tmin) & (tt <= tmax) & (alpha >= 0.0f) & (alpha <= 1.0f) &
-           (beta >= 0.0f) & (beta <= 1.0f);
-  }
-#endif
   if (fabsf(denom) >= 1e-8f) {
     float tt = (a.w - pt_dot(n, o)) / denom;
     if (pt_all2(tt >= tmin, tt <= tmax)) {
@@ -241,7 +197,6 @@ __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const
 
 __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o, pt_v3 d, float tmin,
                                            float tmax, float& t) {
-#if PTMI_LEAF_PRELOAD
   // all 64 B in one round trip (the compiler otherwise sinks the loads into
   // the branches: three dependent L2 round trips per quad test)
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
@@ -249,9 +204,6 @@ __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o
   asm volatile("" : "+v"(A), "+v"(B), "+v"(C), "+v"(E));
   return hit_quad_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
                     make_float4(C.x, C.y, C.z, C.w), make_float4(E.x, E.y, E.z, E.w), o, d, tmin, tmax, t);
-#else
-  return hit_quad_v(q[0], q[1], q[2], q[3], o, d, tmin, tmax, t);
-#endif
 }
 
 __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const float4 c, pt_v3 o, pt_v3 d,
@@ -259,19 +211,6 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
   pt_v3 v0 = pt_v3f(a.x, a.y, a.z), e1 = pt_v3f(a.w, b.x, b.y), e2 = pt_v3f(b.z, b.w, c.x);
   pt_v3 hv = pt_cross(d, e2);
   float det = pt_dot(e1, hv);
-#if PTMI_LEAF_FLAT & 1
-  {
-    const float inv = 1.0f / det;
-    const pt_v3 sv = pt_sub(o, v0);
-    const float u = inv * pt_dot(sv, hv);
-    const pt_v3 q = pt_cross(sv, e1);
-    const float v = inv * pt_dot(d, q);
-    const float tt = inv * pt_dot(e2, q);
-    t = tt;
-    return (fabsf(det) >= 1e-8f) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f) & (tt >= tmin) &
-           (tt <= tmax);
-  }
-#endif
   if (fabsf(det) >= 1e-8f) {
     float inv = 1.0f / det;
     pt_v3 s = pt_sub(o, v0);
@@ -290,15 +229,11 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
 
 __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
                                           float tmax, float& t) {
-#if PTMI_LEAF_PRELOAD
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
   pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1], C = ((const pt_f4*)tr)[2];
   asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
   return hit_tri_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
                    make_float4(C.x, C.y, C.z, C.w), o, d, tmin, tmax, t);
-#else
-  return hit_tri_v(tr[0], tr[1], tr[2], o, d, tmin, tmax, t);
-#endif
 }
 
 __device__ __forceinline__ bool hit_leaf(const DevScene& sc, int32_t ref, pt_v3 o, pt_v3 d, float tmin,
@@ -341,9 +276,7 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // Node layout (include/ptmi.h): the two children's box coordinates are
 // interleaved per component — {lo.x L,R | lo.y L,R}{lo.z L,R | hi.x L,R}
 // {hi.y L,R | hi.z L,R}{ref L, ref R, -, -} — so both children's slabs and
-// centre distances are computed as pairs (pt_f2): scalar f32 ops by default,
-// v_pk_add/v_pk_mul with PTMI_TRAV_SCALAR 0 (IEEE f32 per half either way, so
-// every value is bit-identical to the scalar restatement).
+// centre distances are computed as pairs (pt_f2) of scalar f32 ops.
 //
 // A/B history on MI355X (all parity-identical): near-child shortcut with a
 // nested pop loop -17 %; top of stack in registers +0-2 % (mk) / -3 % (wf);
@@ -355,26 +288,18 @@ __device__ __forceinline__ pt_v3 hit_normal(const DevScene& sc, int32_t ref, pt_
 // pops -11 to -13 % (profiles/r02/ab/ab_trav_prefetch.log). Kept: child
 // pairs (scalar since round 2), precomputed centres, branch-free pushes.
 
-#ifndef PTMI_TRAV_SCALAR
-// The node step's child pairs as two scalar f32 ops (1) or one v_pk_*_f32
-// (0). A packed f32 op costs a wave about the issue time of the two scalar
-// ops it replaces (MI355X_MICROARCH.md constants, 'vector-instruction ISSUE
-// cost' and the packed-f32 filler row), and the pairs need operand shuffles.
-// A/B on MI355X, parity-identical, after -fno-slp-vectorize: C2 +5.5 %,
-// C3 and C4 within noise (profiles/r02/ab/ab_trav_scalar.log). Round 1
-// measured the packed form +2-3 % with SLP packing the scalar form itself.
-#define PTMI_TRAV_SCALAR 1
-#endif
-#if PTMI_TRAV_SCALAR
+// The node step's child pairs are two scalar f32 ops, not one v_pk_*_f32: a
+// packed f32 op costs a wave about the issue time of the two scalar ops it
+// replaces (MI355X_MICROARCH.md constants, 'vector-instruction ISSUE cost' and
+// the packed-f32 filler row), and the pairs need operand shuffles. A/B on
+// MI355X, parity-identical, after -fno-slp-vectorize: C2 +5.5 %, C3 and C4
+// within noise (profiles/r02/ab/ab_trav_scalar.log).
 struct pt_f2 {
   float x, y;
 };
 __device__ __forceinline__ pt_f2 operator+(pt_f2 a, pt_f2 b) { return pt_f2{a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ pt_f2 operator-(pt_f2 a, pt_f2 b) { return pt_f2{a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ pt_f2 operator*(pt_f2 a, pt_f2 b) { return pt_f2{a.x * b.x, a.y * b.y}; }
-#else
-typedef float pt_f2 __attribute__((ext_vector_type(2)));
-#endif
 
 struct Stack {
   uint2* slot0;  // &lds[tid]; slot k at slot0[k * SB] (SB = threads per block)
@@ -415,34 +340,7 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 __device__ unsigned long long g_probe[16];
 #endif
 
-#ifndef PTMI_EARLY_FETCH
-// A/B on MI355X (parity-identical): all of a step's loads issued before any
-// test, one wait per step: -4 % mk C2, -3 % mk C4, -1 % wf
-// (profiles/r01/ab_early_fetch.log)
-#define PTMI_EARLY_FETCH 0
-#endif
-#ifndef PTMI_NODE_CENTRES
-#define PTMI_NODE_CENTRES 1
-#endif
-
-#ifndef PTMI_TRAV2
-// Two-level node packets (include/ptmi.h, PTMI_NODE_BYTES): a popped node's
-// packet also holds both children's child records, so the step that expands
-// a node expands its near child in the same round trip (see trav_step).
-#define PTMI_TRAV2 0
-#endif
-#if PTMI_TRAV2
-constexpr uint32_t kNodeBytes = 256;
-#else
 constexpr uint32_t kNodeBytes = 80;
-#endif
-
-#ifndef PTMI_NODES_SGPR
-#define PTMI_NODES_SGPR 1  // megakernel: node base pinned in SGPRs (A/B with leaf preload: +0.8 % C2/C4)
-#endif
-#ifndef PTMI_NODES_VGPR
-#define PTMI_NODES_VGPR (!PTMI_NODES_SGPR)  // A/B on MI355X: +2 % megakernel
-#endif
 
 // In-flight traversal of one ray: begin (root test, push root) and one pop
 // of the loop per step, so a kernel can interleave steps of different rays'
@@ -480,108 +378,6 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
   }
 }
 
-#if PTMI_TRAV2
-// Slab entry/exit of both children of one 80-B child record and their
-// projected centre distances (kernels.py:600-621, 707-713), as packed pairs.
-struct PairHit {
-  float E0, X0, E1, X1, d0, d1;
-};
-typedef float pt_f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ PairHit pair_hit(const pt_f4v A, const pt_f4v B, const pt_f4v C, const pt_f4v R,
-                                            const pt_f4v Cxy, pt_f2 ox, pt_f2 oy, pt_f2 oz, pt_f2 ix, pt_f2 iy,
-                                            pt_f2 iz, pt_f2 dx, pt_f2 dy, pt_f2 dz, float tmin) {
-  const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
-  const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
-  const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
-  const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
-  const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
-  PairHit h;
-  h.E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
-  h.X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
-  h.E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
-  h.X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
-  const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
-  const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
-  h.d0 = dist.x;
-  h.d1 = dist.y;
-  return h;
-}
-
-// Expansion of a popped internal node P from its 256-B packet: record 0 holds
-// P's children (c0, c1), records 1 and 2 hold c0's and c1's children. The
-// reference (kernels.py:698-740) pushes P's far child, then its near child,
-// and pops the near child at once: with the same closest_t it tests the near
-// box against [t_min, closest_t] and, if internal and hit, pushes the near
-// child's far and near children. This step does exactly that in one round
-// trip: it pushes P's far child and then the near child's two children (or
-// the near child itself when it is a leaf). The stack holds the reference's
-// entries in the reference's order minus the near child's own entry, so
-// pops, culls and ties are unchanged, and the stack is never deeper than the
-// reference's (an expanded near child at depth d + 1 has children at depth
-// d + 2 <= max_leaf_depth: its three writes end at slot <= max_leaf_depth).
-template <int STACK, int SB>
-__device__ __forceinline__ void trav_expand2(const __attribute__((address_space(1))) pt_f4v* nodes, Trav& tr,
-                                             pt_v3 o, pt_v3 d, int32_t ref) {
-  typedef const __attribute__((address_space(1))) pt_f4v gf4;
-  constexpr uint32_t kSlot = SB * 8;
-  gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);
-#if PTMI_TRAV2 == 2
-  // record 0 only; the near child's record is loaded once the near child is
-  // known (a second, cache-hot round trip from the same packet, instead of
-  // holding both children's records in registers)
-  pt_f4v P[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) P[k] = nd[k];
-#else
-  pt_f4v P[15];
-#pragma unroll
-  for (int k = 0; k < 15; ++k) P[k] = nd[k];
-#endif
-  const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
-  const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
-  const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
-  const float tmin = tr.tmin;
-  const PairHit h = pair_hit(P[0], P[1], P[2], P[3], P[4], ox, oy, oz, ix, iy, iz, dx, dy, dz, tmin);
-  const bool ln = h.d0 < h.d1;  // child 0 is the near one
-  const int32_t ref0 = __float_as_int(P[3].x), ref1 = __float_as_int(P[3].y);
-  const int32_t nref = ln ? ref0 : ref1, fref = ln ? ref1 : ref0;
-  const float nE = ln ? h.E0 : h.E1, fE = ln ? h.E1 : h.E0;
-  const bool nh = ln ? (h.X0 >= h.E0) : (h.X1 >= h.E1), fh = ln ? (h.X1 >= h.E1) : (h.X0 >= h.E0);
-  // the near child's pop, right after P's expansion: box hit and E <= closest_t
-  const bool coll = nh && nref >= 0 && nE <= tr.closest;
-  pt_f4v NA, NB, NC, NR, NCxy;
-#if PTMI_TRAV2 == 2
-  {
-    gf4* nn = nd + (ln ? 5 : 10);
-    NA = nn[0]; NB = nn[1]; NC = nn[2]; NR = nn[3]; NCxy = nn[4];
-  }
-#else
-  NA = ln ? P[5] : P[10];
-  NB = ln ? P[6] : P[11];
-  NC = ln ? P[7] : P[12];
-  NR = ln ? P[8] : P[13];
-  NCxy = ln ? P[9] : P[14];
-#endif
-  const PairHit g = pair_hit(NA, NB, NC, NR, NCxy, ox, oy, oz, ix, iy, iz, dx, dy, dz, tmin);
-  const bool gl = g.d0 < g.d1;
-  const int32_t g0 = __float_as_int(NR.x), g1 = __float_as_int(NR.y);
-  // entries above P's far child: the near child's far and near children, or the near child itself
-  const int32_t r2 = coll ? (gl ? g1 : g0) : nref;
-  const float e2 = coll ? (gl ? g.E1 : g.E0) : nE;
-  const bool b2 = coll ? (gl ? (g.X1 >= g.E1) : (g.X0 >= g.E0)) : nh;
-  const int32_t r3 = gl ? g0 : g1;
-  const float e3 = gl ? g.E0 : g.E1;
-  const bool b3 = coll && (gl ? (g.X0 >= g.E0) : (g.X1 >= g.E1));
-  const uint32_t s1 = tr.sp;
-  const uint32_t s2 = s1 + (fh ? kSlot : 0u);
-  const uint32_t s3 = s2 + (b2 ? kSlot : 0u);
-  lds_store2(s1, (uint32_t)fref, __float_as_uint(fE));
-  lds_store2(s2, (uint32_t)r2, __float_as_uint(e2));
-  if (coll) lds_store2(s3, (uint32_t)r3, __float_as_uint(e3));
-  tr.sp = s3 + (b3 ? kSlot : 0u);
-}
-#endif
-
 // One step of the traversal loop (one pop); precondition tr.busy().
 // A/B on MI355X (parity-identical): deferring a popped leaf's test to the next
 // step -5 % mk / -3.5 % wf; testing a just-pushed leaf in the expanding step
@@ -591,9 +387,13 @@ __device__ __forceinline__ void trav_expand2(const __attribute__((address_space(
 // faster (-0.5 %; profiles/r01/ab_fast_div_sqrt.log). One 80-B fetch per
 // popped entry, node or primitive, issued before the node/leaf branch (one
 // L2 wait per mixed step instead of two): -4.6 % mk, -14 % wf
-// (profiles/r01/ab_unified_fetch.log). Node stride 128 B (one node per
-// line) -5 %; 64-B nodes with x/y centres computed +0.4 % (noise), kept at
-// 80 B (profiles/r01/ab_node_layout.log).
+// (profiles/r01/ab_unified_fetch.log); each lane's own entry load (node,
+// sphere, quad or triangle) issued before any test, one wait per step, -4 %
+// mk / -1 % wf (profiles/r01/ab_early_fetch.log). Node stride 128 B (one node
+// per line) -5 %; 64-B nodes with x/y centres computed +0.4 % (noise), kept at
+// 80 B (profiles/r01/ab_node_layout.log). Two-level 256-B node packets (a
+// node's children and grandchildren, the near child expanded in the same
+// step) -20 to -43 % (profiles/r02/ab/ab_trav2_packets.log).
 template <int STACK, int SB = kBlock>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
@@ -602,12 +402,6 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) pt_f4 gf4;
   gf4* nodes = (gf4*)node_base;
-#if PTMI_NODES_VGPR
-  // keep the node base in VGPRs: under SGPR pressure the compiler otherwise
-  // re-loads it from the kernarg segment on every visit (s_load + lgkmcnt wait
-  // on the pop's critical path)
-  asm volatile("" : "+v"(nodes));
-#endif
   constexpr uint32_t kSlot = SB * 8;  // bytes between a lane's consecutive slots
   tr.sp -= kSlot;
   const pt_u2v ent = lds_load2(tr.sp);
@@ -620,46 +414,6 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
 #endif
 #endif
   if (!(__uint_as_float(ent.y) <= tr.closest)) return;
-#if PTMI_EARLY_FETCH
-  // Every popping lane issues its own entry's load (80-B node, 16-B sphere,
-  // 64-B quad, 48-B triangle) into the same registers before any test runs,
-  // and the wave waits once: a step mixing node, sphere and quad lanes pays
-  // one L2 round trip instead of one per branch.
-  pt_f4 F0, F1, F2, F3, F4;
-  if (ref >= 0) {
-    gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);
-    F0 = nd[0]; F1 = nd[1]; F2 = nd[2]; F3 = nd[3]; F4 = nd[4];
-  } else {
-    const int32_t ty = leaf_type(ref), ix = leaf_index(ref);
-    if (ty == kSphere) {
-      F0 = ((const gf4*)sc.spheres)[ix];
-    } else if (ty == kQuad) {
-      gf4* q = (const gf4*)sc.quads + 4 * ix;
-      F0 = q[0]; F1 = q[1]; F2 = q[2]; F3 = q[3];
-    } else {
-      gf4* tq = (const gf4*)sc.tris + 3 * ix;
-      F0 = tq[0]; F1 = tq[1]; F2 = tq[2];
-    }
-  }
-  asm volatile("" : "+v"(F0), "+v"(F1), "+v"(F2), "+v"(F3), "+v"(F4));
-  if (ref < 0) {
-    const int32_t ty = leaf_type(ref);
-#if PTMI_PROBE == 2
-    tr.probe |= ty == kSphere ? 1 : 2;
-#endif
-    const float4 a = make_float4(F0.x, F0.y, F0.z, F0.w), b = make_float4(F1.x, F1.y, F1.z, F1.w);
-    const float4 c = make_float4(F2.x, F2.y, F2.z, F2.w), e = make_float4(F3.x, F3.y, F3.z, F3.w);
-    float t;  // leaf: kernels.py:671-697
-    const bool h = ty == kSphere ? hit_sphere_t(a, o, d, tr.tmin, tr.closest, t)
-                   : ty == kQuad ? hit_quad_v(a, b, c, e, o, d, tr.tmin, tr.closest, t)
-                                 : hit_tri_v(a, b, c, o, d, tr.tmin, tr.closest, t);
-    if (h && t < tr.closest) {
-      tr.closest = t;
-      tr.best = ref;
-    }
-    return;
-  }
-#else
   if (ref < 0) {
 #if PTMI_PROBE == 2
     tr.probe |= leaf_type(ref) == kSphere ? 1 : 2;
@@ -671,7 +425,6 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     }
     return;
   }
-#endif
 #if PTMI_PROBE == 2
   tr.probe |= 4;
 #endif
@@ -688,21 +441,13 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     }
   }
 #endif
-#if PTMI_TRAV2
-  trav_expand2<STACK, SB>(nodes, tr, o, d, ref);
-  return;
-#endif
   // internal: kernels.py:698-740, both children at once
   const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
   const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
   const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
   const float tmin = tr.tmin;
-#if PTMI_EARLY_FETCH
-  const pt_f4 A = F0, B = F1, C = F2, R = F3;
-#else
   gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // 80-B node at byte offset ref
   const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
-#endif
   const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
   const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
   const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
@@ -713,17 +458,8 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
   const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
   // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
-#if PTMI_NODE_CENTRES
-#if PTMI_EARLY_FETCH
-  const pt_f4 Cxy = F4;
-#else
   const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
-#endif
   const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
-#else
-  const pt_f2 half = pt_f2s(0.5f);
-  const pt_f2 cx = (lox + hix) * half, cy = (loy + hiy) * half, cz = (loz + hiz) * half;
-#endif
   const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
   const bool ln = dist.x < dist.y;  // child 0 is the near one; the far child is pushed first
   const bool h0 = X0 >= E0, h1 = X1 >= E1;

@@ -13,13 +13,12 @@
 //   * direct mode: the accumulator is read once and written once per launch
 //     (sample colours added in sample order in registers: same float
 //     sequence as accum += color per sample);
-//   * staged mode (the default for multi-sample calls): work units are
-//     (tile, chunk of samples), many more than the chip holds at once, so the
-//     launch does not end in a long partially-filled last round of blocks
-//     (one unit per tile left ~30 % of the chip idle in the tail); each path
-//     writes its colour to staging[sample][pixel] and stage_resolve adds
-//     them in sample order — the same float additions as direct mode;
-//   * BVH: child-box BVH2 nodes (64 B, one node load tests both children),
+//   * staged mode (the default for multi-sample calls): persistent waves
+//     draw (8x8 tile, sample) units from sharded counters, so the launch
+//     does not end in a long partially-filled last round of blocks; each
+//     path writes its colour to staging[sample][pixel] and stage_resolve
+//     adds them in sample order — the same float additions as direct mode;
+//   * BVH: child-box BVH2 nodes (80 B, one node load tests both children),
 //     traversal stack in LDS (slot-major, conflict-free), see pt_device.hpp.
 // Perlin corner loop fully unrolled here (A/B on MI355X: +2.5 % megakernel,
 // where it costs no occupancy); the wavefront shade kernel keeps it rolled.
@@ -84,32 +83,19 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #ifndef PTMI_MK_PRIO_SHADE
 #define PTMI_MK_PRIO_SHADE 0
 #endif
-#ifndef PTMI_MK_HOLD_NOISE
-#define PTMI_MK_HOLD_NOISE 0  // A/B: 4 or 8 held lanes -1 to -1.5 % (profiles/r01/ab_mk_hold_noise.log)
-#endif
-#ifndef PTMI_MK_NT
-#define PTMI_MK_NT 0
-#endif
-#ifndef PTMI_MK_ONE_RUV
-// One random_unit_vector call site per shading round (scatter_begin /
-// scatter_end, pt_device.hpp): metal, isotropic and constant-medium lanes draw
-// their unit vectors in one rejection loop. A/B on MI355X, parity-identical:
-// C2 -1.1 %, C4 +0.4 % (profiles/r02/ab/ab_one_scatter.log); off here, on in
-// the wavefront's wf_medium (PTMI_WF_ONE_SCATTER).
-#define PTMI_MK_ONE_RUV 0
-#endif
-#ifndef PTMI_MK_KEEP_SLOT
-// Staged mode: the path's staging slot is computed when its item is bound and
-// kept in a register, instead of decoding the item again when the path ends.
-#define PTMI_MK_KEEP_SLOT 1  // A/B: C2 +0.8 %, C4 +1 % (profiles/r02/ab/ab_one_scatter.log)
-#endif
-#ifndef PTMI_MK_ONE_BEGIN
-// One trav_begin call site per pass of the outer loop: lanes continuing a path
-// and lanes starting one (refill) mark need_seg and begin together after the
-// refill, instead of two divergent copies of trav_begin (3 divisions + the
-// root slab) in one shading round.
-#define PTMI_MK_ONE_BEGIN 1
-#endif
+// A/B, not kept (profiles/): Perlin-textured hits held until 4 or 8 of a wave
+// are ready, -1 to -1.5 % (r01/ab_mk_hold_noise.log); non-temporal staging
+// stores, +-0.3 % (r02/ab/ab_nontemporal.log); one random_unit_vector site per
+// shading round (the wavefront's wf_medium keeps it), C2 -1.1 %
+// (r02/ab/ab_one_scatter.log); the unit fetch's shard loop kept rolled,
+// -0.6 to -1.1 % (r02/ab/ab_mk_fetch_rolled.log).
+// Staged mode keeps the path's staging slot, computed when its item is bound,
+// in a register instead of decoding the item again when the path ends (A/B:
+// C2 +0.8 %, C4 +1 %; profiles/r02/ab/ab_one_scatter.log). Lanes continuing
+// a path and lanes starting one (refill) mark need_seg and begin together
+// after the refill: one trav_begin call site per pass of the outer loop
+// instead of two divergent copies (3 divisions + the root slab) in one
+// shading round (C2 +1.6 %, C4 +2.3 %; profiles/r02/ab/ab_mk_one_begin.log).
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -130,11 +116,9 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_MIN_WAVES_16 5
 #endif
 
-// Block = PTMI_MK_BLOCK_WAVES waves: 4 -> a 16x16 pixel tile, 1 -> 8x8.
-#ifndef PTMI_MK_BLOCK_WAVES
-#define PTMI_MK_BLOCK_WAVES 1  // A/B on MI355X: 1-wave blocks +7 % (C2) / +12 % (C4): a finished wave frees its slot at once
-#endif
-constexpr int kMkBlock = 64 * PTMI_MK_BLOCK_WAVES;
+// One-wave blocks, each an 8x8 pixel tile (A/B on MI355X: +7 % C2 / +12 % C4
+// over 4-wave 16x16 blocks: a finished wave frees its slot at once).
+constexpr int kMkBlock = 64;
 
 // Staged mode, persistent waves: the grid is one round of the chip's wave
 // slots and every wave draws 64-item units (one 8x8 tile x one sample) from a
@@ -144,9 +128,6 @@ constexpr int kMkBlock = 64 * PTMI_MK_BLOCK_WAVES;
 // PTMI_MK_CHUNK_SAMPLES units while plenty are left, fewer in the tail, so a
 // wave changes tile rarely (lanes of two tiles in one wave fetch more distinct
 // cache lines per load) and the last fetches are small.
-#ifndef PTMI_MK_PERSIST
-#define PTMI_MK_PERSIST 1
-#endif
 #ifndef PTMI_MK_CHUNK_SAMPLES
 #define PTMI_MK_CHUNK_SAMPLES 32  // A/B (C2, C4): 32/4 ~ 16/4 ~ 64/4 > 16/2, 16/8, 8/4 >> 64/2
 #endif
@@ -184,15 +165,6 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return 
 // one counter 2448 (2479), 8 contiguous shards 2320 (2546), 8 interleaved
 // 2560 (2597), 4 interleaved 2552 (2590) Msamples/s; 16-spp calls 1954 ->
 // 2324 (profiles/r02/ab/ab_mk_shards.log).
-#ifndef PTMI_MK_FETCH_ROLLED
-// The shard loop of a unit fetch kept rolled: unrolled, its 8 counter
-// addresses and bounds are hoisted out of the persistent loop into SGPRs,
-// which then spill to VGPR lanes (47 SGPR spills in the 16-slot kernel).
-#define PTMI_MK_FETCH_ROLLED 0
-#endif
-#ifndef PTMI_MK_SHARD_INTERLEAVE
-#define PTMI_MK_SHARD_INTERLEAVE 1
-#endif
 constexpr int kMkShards = PTMI_MK_SHARDS;
 constexpr int kMkCtlLine = 64;  // int32 words per 256-B counter line
 
@@ -206,8 +178,7 @@ struct MkWork {
   int32_t nunits;    // units of the batch (multiple of csamp)
   int32_t tail_div;  // TAIL_DIV * waves of the grid
 };
-constexpr int kMkTile = PTMI_MK_BLOCK_WAVES == 4 ? 16 : 8;
-static_assert(PTMI_MK_BLOCK_WAVES == 4 || PTMI_MK_BLOCK_WAVES == 1, "block = 1 or 4 waves");
+constexpr int kMkTile = 8;
 
 template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
@@ -218,9 +189,8 @@ template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && STACK < 20) ? PTMI_MK_MIN_WAVES_16 : STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
-  constexpr bool kPersist = STAGED && PTMI_MK_PERSIST;
+  constexpr bool kPersist = STAGED;  // staged launches are persistent
   const float4* nodes = sc.nodes;
-#if PTMI_NODES_SGPR
   {  // node base pinned in an SGPR pair for the whole kernel: under SGPR
      // pressure the compiler otherwise re-loads it from the kernarg segment on
      // every traversal step (s_load + lgkmcnt wait on the pop's critical path)
@@ -229,39 +199,35 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     asm volatile("" : "+s"(lo), "+s"(hi));
     nodes = (const float4*)(((uint64_t)hi << 32) | lo);
   }
-#endif
   __shared__ uint2 lds_stack[STACK * kMkBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
 
   // each wave renders an 8x8 pixel square (square footprints keep a wave's
-  // camera rays coherent in the BVH); a 4-wave block covers 16x16.
-  const int lane = tid & 63, wv = tid >> 6;
-  const int32_t sq_x = fr.x0 + (int32_t)blockIdx.x * kMkTile + ((wv & 1) << 3);  // the wave's square
-  const int32_t sq_y = (int32_t)blockIdx.y * kMkTile + ((wv >> 1) << 3);          // (local rows)
+  // camera rays coherent in the BVH)
+  const int lane = tid & 63;
+  const int32_t sq_x = fr.x0 + (int32_t)blockIdx.x * kMkTile;  // the wave's square
+  const int32_t sq_y = (int32_t)blockIdx.y * kMkTile;          // (local rows)
   const size_t npix = (size_t)fr.w * (size_t)fr.n_rows;
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
   uint32_t n_seg = 0, n_med = 0, n_paths = 0;  // per-thread counts of one launch
+  uint32_t n_rr = 0, n_cap = 0;                 // paths ended by Russian roulette / by the depth cap
   PathState ps;
 
   // Work of the wave. Direct mode: lane L owns pixel L of the square for all
   // samples of the call (its accumulator lives in registers). Staged mode:
-  // the wave's (sample, pixel) items, sample-major, are handed out to lanes
-  // as their paths end (ballot + mbcnt, a wave-private counter: no atomics),
-  // so all 64 lanes stay busy until the wave's last few paths; any lane may
-  // render any item, because colours go to staging[sample][pixel].
-  int32_t s0 = s_begin, ns = s_count;
-  if (STAGED && !kPersist) {
-    s0 = s_begin + (int32_t)blockIdx.z * chunk;
-    ns = min(chunk, s_begin + s_count - s0);
-  }
+  // the wave's (sample, pixel) items are handed out to lanes as their paths
+  // end (ballot + mbcnt), so all 64 lanes stay busy until the wave's last few
+  // paths; any lane may render any item, because colours go to
+  // staging[sample][pixel].
+  const int32_t s0 = s_begin, ns = s_count;
   const uint32_t total = 64u * (uint32_t)ns;
   uint32_t next = 64u;  // wave-uniform: next unassigned item
   uint32_t item = (uint32_t)lane;
   uint32_t wend = 0u;   // persistent: end of the wave's current units (items)
   bool drained = false; // persistent: the batch's units are all handed out
   int32_t px = 0, py = -1, lr = 0, s = s0;
-  uint32_t slot = 0u;  // PTMI_MK_KEEP_SLOT: staging slot of the bound item
+  uint32_t slot = 0u;  // staging slot of the bound item
   float* ap = nullptr;
   pt_v3 acc = pt_v3f(0.0f, 0.0f, 0.0f);
   bool live = false;
@@ -273,17 +239,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   };
   auto locate = [&](uint32_t k) -> Loc {
     if (kPersist) {
-#if PTMI_MK_SHARD_INTERLEAVE
       // shard-contiguous unit numbering: shard s holds tiles s, s + S, s + 2S, ...
       const uint32_t v = k >> 6, sh = fdiv(v, wk.by_len), j = v - sh * (uint32_t)wk.shard_len;
       const uint32_t tq = fdiv(j, wk.by_nb), t = tq * (uint32_t)kMkShards + sh, ty = fdiv(t, wk.by_tiles_x);
       return Loc{fr.x0 + (int32_t)(t - ty * (uint32_t)wk.tiles_x) * 8, (int32_t)ty * 8,
                  s_begin + (int32_t)(j - tq * (uint32_t)wk.nb)};
-#else
-      const uint32_t u = k >> 6, t = fdiv(u, wk.by_nb), ty = fdiv(t, wk.by_tiles_x);
-      return Loc{fr.x0 + (int32_t)(t - ty * (uint32_t)wk.tiles_x) * 8, (int32_t)ty * 8,
-                 s_begin + (int32_t)(u - t * (uint32_t)wk.nb)};
-#endif
     }
     return Loc{sq_x, sq_y, s0 + (int32_t)(k >> 6)};
   };
@@ -294,9 +254,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     px = l.x + (p & 7);
     lr = l.row + (p >> 3);
     py = (lr < fr.n_rows && px < fr.x0 + fr.w && s < s_begin + s_count) ? frame_row(fr, lr) : -1;
-#if PTMI_MK_KEEP_SLOT
     if (STAGED) slot = (uint32_t)(s - s_begin) * (uint32_t)npix + (uint32_t)lr * (uint32_t)fr.w + (uint32_t)(px - fr.x0);
-#endif
     return py >= 0;
   };
   if (kPersist) {  // first units of the wave
@@ -323,8 +281,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   typename TravOf<TRAV>::T tr;
   tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
-  bool hold = false;  // PTMI_MK_HOLD_NOISE: a traced Perlin-textured hit waiting for more of its kind
-  bool need_seg = false;  // PTMI_MK_ONE_BEGIN: begin a segment after this pass's refill
+  bool need_seg = false;  // begin a segment after this pass's refill
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
     trav_begin<STACK, kMkBlock>(sc, tr, st, ps.dir, ps.o, em ? ps.t_entry + 0.0001f : kTMin, kTMax);  // :418/:1057
@@ -349,7 +306,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      if (nbusy <= (uint32_t)(STACK > 16 ? PTMI_MK_SHADE_AT_DEEP : PTMI_MK_SHADE_AT) && pt_ballot(trav && !tr.busy() && !hold) != 0ull) break;
+      if (nbusy <= (uint32_t)(STACK > 16 ? PTMI_MK_SHADE_AT_DEEP : PTMI_MK_SHADE_AT) && pt_ballot(trav && !tr.busy()) != 0ull) break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -375,21 +332,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #if PTMI_MK_PRIO_TRAV >= 0
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
-#if PTMI_MK_HOLD_NOISE
-    {  // Perlin-textured surface hits wait (lane idle) until PTMI_MK_HOLD_NOISE of them are
-       // ready or no lane is still traversing, so the wave pays the turbulence's table round
-       // trips once for several lanes (A/B knob)
-      bool nr = false;
-      if (trav && !tr.busy() && ps.mode != kModeMediumExit && tr.any()) {
-        const uint32_t fl = mat_flags(sc, mat_index(sc, tr.best));
-        nr = ((fl >> 4) & 0xfu) == 3u && ((fl & 0xfu) == 0u || (fl & 0xfu) == 4u) && !((fl >> 8) & 1u);
-      }
-      const unsigned long long mn = pt_ballot(nr);
-      const uint32_t nn = __builtin_popcount((uint32_t)mn) + __builtin_popcount((uint32_t)(mn >> 32));
-      hold = nr && nn < (uint32_t)PTMI_MK_HOLD_NOISE && pt_ballot(tr.busy()) != 0ull;
-    }
-#endif
-    if (trav && !tr.busy() && !hold) {  // segment traced: shade it
+    if (trav && !tr.busy()) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
       const bool hit = tr.any();
@@ -398,9 +341,6 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 
       bool done = false, scattered = false, passthrough = false, to_medium = false;
       pt_v3 hp, sdir, att;
-#if PTMI_MK_ONE_RUV
-      int32_t ruv = kRuvNone;
-#endif
       int32_t g = -1;
       if (!exit_mode) {
         if (!hit) {
@@ -430,11 +370,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           // apply_constant_medium, kernels.py:421-448 (density m3.w)
           if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
             hp = mp;  // kernels.py:1082-1097
-#if PTMI_MK_ONE_RUV
-            ruv = kRuvMedium;
-#else
             sdir = random_unit_vector(ps.rng);
-#endif
             att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
             scattered = true;
           } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
@@ -448,27 +384,12 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
             st = ps.t_entry;
           }
         }
-#if PTMI_MK_ONE_RUV
-        pt_v3 n;
-        if (surface) {  // kernels.py:1120-1128
-          hp = pt_add(ps.o, pt_scale(ps.dir, st));
-          n = hit_normal(sc, sref, hp, ps.dir);
-          ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
-          ruv = scatter_begin(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att, scattered);
-        }
-        if (ruv != kRuvNone) {  // the round's one random_unit_vector site
-          const pt_v3 v = random_unit_vector(ps.rng);
-          if (ruv == kRuvMedium) sdir = v;
-          else scattered = scatter_end(sc, ruv, sref, m, hp, n, v, sdir, att);
-        }
-#else
         if (surface) {  // kernels.py:1120-1128
           hp = pt_add(ps.o, pt_scale(ps.dir, st));
           pt_v3 n = hit_normal(sc, sref, hp, ps.dir);
           ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
           scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
         }
-#endif
       }
 
       if (!done && !to_medium) {
@@ -478,17 +399,25 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           ps.thr = pt_mul(ps.thr, att);
           if (ps.depth + 1 >= fr.max_depth) {
             done = true;
+            ++n_cap;
           } else {
             if (ps.depth + 1 >= kRRMinDepth) {
               float sp = pt_minf(pt_maxf(pt_maxf(ps.thr.x, ps.thr.y), ps.thr.z), kRRMaxProb);
-              if (ps.rng.next() > sp) done = true;
-              else ps.thr = pt_divs(ps.thr, sp);
+              if (ps.rng.next() > sp) {
+                done = true;
+                ++n_rr;
+              } else {
+                ps.thr = pt_divs(ps.thr, sp);
+              }
             }
             if (!done) ++ps.depth;
           }
         } else if (passthrough) {
           ++ps.depth;
-          if (ps.depth >= fr.max_depth) done = true;
+          if (ps.depth >= fr.max_depth) {
+            done = true;
+            ++n_cap;
+          }
         } else {
           done = true;
         }
@@ -496,26 +425,10 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       if (done) {
         ++n_paths;
         if (STAGED) {  // staging[s][p]; stage_resolve adds them in sample order
-#if PTMI_MK_KEEP_SLOT
           float* o = staging + 3 * (size_t)slot;
-#else
-          // slot of this lane's item (recomputed: pixel/sample need not stay live)
-          const int32_t ip = (int32_t)(item & 63u);
-          const Loc l = locate(item);
-          const size_t srel = (size_t)(l.s - s_begin);
-          float* o = staging + 3 * (srel * npix + (size_t)(l.row + (ip >> 3)) * (size_t)fr.w +
-                                    (size_t)(l.x + (ip & 7) - fr.x0));
-#endif
-#if PTMI_MK_NT
-          // A/B knob: non-temporal staging stores, +-0.3 % (profiles/r02/ab/ab_nontemporal.log)
-          __builtin_nontemporal_store(ps.color.x, o);
-          __builtin_nontemporal_store(ps.color.y, o + 1);
-          __builtin_nontemporal_store(ps.color.z, o + 2);
-#else
           o[0] = ps.color.x;
           o[1] = ps.color.y;
           o[2] = ps.color.z;
-#endif
           live = false;
         } else {  // render_sample: accum += color (kernels.py:1187), next sample of the same pixel
           acc = pt_add(acc, ps.color);
@@ -523,19 +436,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           live = s < s0 + ns;
           if (live) {
             start_path(fr, px, py, s, ps);
-#if PTMI_MK_ONE_BEGIN
             need_seg = true;
-#else
-            begin_segment();
-#endif
           }
         }
       } else {
-#if PTMI_MK_ONE_BEGIN
         need_seg = true;  // next segment of this path (or its medium exit search)
-#else
-        begin_segment();  // next segment of this path (or its medium exit search)
-#endif
       }
     }
     if (kPersist) {  // hand the wave's next items to the lanes without a path, fetching units as needed
@@ -550,9 +455,6 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           int32_t u0 = 0;
           if (lane == 0) {
             u0 = -1;
-#if PTMI_MK_FETCH_ROLLED
-#pragma unroll 1
-#endif
             for (int a = 0; a < kMkShards; ++a) {  // home shard first, then steal
               const int32_t sh = (int32_t)((blockIdx.x + (unsigned)a) % (unsigned)kMkShards);
               const int32_t lo = sh * wk.shard_len, hi = min(lo + wk.shard_len, wk.nunits);
@@ -586,20 +488,14 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           if (bind(item)) {
             start_path(fr, px, py, s, ps);
             live = true;
-#if PTMI_MK_ONE_BEGIN
             need_seg = true;
-#else
-            begin_segment();
-#endif
           }
         }
       }
-#if PTMI_MK_ONE_BEGIN
       if (need_seg) {
         need_seg = false;
         begin_segment();
       }
-#endif
 #if PTMI_PROBE == 2
       {
         const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -608,39 +504,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       }
 #endif
       if (__ballot(live) == 0ull && drained && next >= wend) break;
-    } else if (STAGED) {  // hand the wave's next items to the lanes without a path
-      const unsigned long long want = __ballot(!live);
-      if (want && next < total) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-        if (!live) {
-          item = next + rank;
-          if (item < total && bind(item)) {
-            start_path(fr, px, py, s, ps);
-            live = true;
-#if PTMI_MK_ONE_BEGIN
-            need_seg = true;
-#else
-            begin_segment();
-#endif
-          }
-        }
-        next += (uint32_t)__popcll(want);
-      }
-#if PTMI_MK_ONE_BEGIN
-      if (need_seg) {
-        need_seg = false;
-        begin_segment();
-      }
-#endif
-      if (__ballot(live) == 0ull && next >= total) break;
     } else {
-#if PTMI_MK_ONE_BEGIN
       if (need_seg) {
         need_seg = false;
         begin_segment();
       }
-#endif
       if (__ballot(live) == 0ull) break;
     }
   }
@@ -662,13 +530,15 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   if (counters) {  // block sums in the (now idle) stack LDS: no extra LDS, 5 blocks/CU fit
     __syncthreads();
     unsigned long long* red = reinterpret_cast<unsigned long long*>(lds_stack);
-    if (tid < 3) red[tid] = 0ull;
+    if (tid < kNumCounters) red[tid] = 0ull;
     __syncthreads();
     atomicAdd(&red[0], (unsigned long long)n_seg);
     atomicAdd(&red[1], (unsigned long long)n_med);
     atomicAdd(&red[2], (unsigned long long)n_paths);
+    atomicAdd(&red[3], (unsigned long long)n_rr);
+    atomicAdd(&red[4], (unsigned long long)n_cap);
     __syncthreads();
-    if (tid < 3) atomicAdd(counters + tid, red[tid]);
+    if (tid < kNumCounters) atomicAdd(counters + tid, red[tid]);
   }
 }
 
@@ -731,13 +601,6 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
 #ifndef PTMI_MK_STAGED_MIN_STACK
 #define PTMI_MK_STAGED_MIN_STACK 16  // staged: STACK 16 scenes use the 16-slot kernel at 5 waves/SIMD (PTMI_MK_MIN_WAVES_16)
 #endif
-#ifndef PTMI_MK_TARGET_BLOCKS
-#define PTMI_MK_TARGET_BLOCKS (16384 * 4 / PTMI_MK_BLOCK_WAVES)  // ~16 rounds of the chip's wave slots
-#endif
-
-#ifndef PTMI_MK_DIRECT_MIN_TILES
-#define PTMI_MK_DIRECT_MIN_TILES 0x7fffffff  // A/B: staged + item pool beat direct even at 4K (+3 %)
-#endif
 
 static size_t mk_staging_bytes(int32_t npix, int32_t batch) {
   return (3 * sizeof(float) * (size_t)npix * (size_t)batch + 255) & ~(size_t)255;
@@ -757,8 +620,6 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   float* accum = nullptr;  // staged kernels write staging only
   const unsigned tx = (unsigned)((fr.w + kMkTile - 1) / kMkTile), ty = (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile);
   const int64_t tiles = (int64_t)tx * ty;
-#if PTMI_MK_PERSIST
-  static_assert(PTMI_MK_BLOCK_WAVES == 1, "persistent staged mode uses one-wave blocks");
   int dev = 0, ncu = 0, per_cu = 0;
   hipError_t e0 = hipGetDevice(&dev);
   if (e0 == hipSuccess) e0 = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -771,17 +632,12 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   wk.tiles_x = (int32_t)tx;
   wk.nb = nb;
   if (tiles * nb * 64 >= (1ll << 32)) return hipErrorInvalidValue;  // item ids are 32-bit
-#if PTMI_MK_SHARD_INTERLEAVE
   // shard s: tiles s, s + S, ... (interleaved across the image, so every shard
   // costs about the same); virtual units past the last tile decode to rows
   // outside the frame and are skipped
   wk.shard_len = (int32_t)((tiles + kMkShards - 1) / kMkShards) * nb;
   wk.nunits = wk.shard_len * kMkShards;
   if ((int64_t)wk.nunits * 64 >= (1ll << 32)) return hipErrorInvalidValue;
-#else
-  wk.nunits = (int32_t)(tiles * nb);
-  wk.shard_len = (wk.nunits + kMkShards - 1) / kMkShards;
-#endif
   wk.by_len = fast_div((uint32_t)wk.shard_len);
   wk.by_nb = fast_div((uint32_t)nb);
   wk.by_tiles_x = fast_div((uint32_t)wk.tiles_x);
@@ -798,17 +654,6 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, nb, staging, counters, wk);
   prof_end(kProfMk, stream);
-#else
-  int64_t nchunks = (PTMI_MK_TARGET_BLOCKS + tiles - 1) / tiles;
-  if (nchunks < 1) nchunks = 1;
-  if (nchunks > nb) nchunks = nb;
-  const int32_t chunk = (int32_t)((nb + nchunks - 1) / nchunks);
-  nchunks = (nb + chunk - 1) / chunk;
-  prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3(tx, ty, (unsigned)nchunks), dim3(kMkBlock), 0, stream,
-                     sc, fr, accum, s_begin, nb, chunk, staging, counters, MkWork{});
-  prof_end(kProfMk, stream);
-#endif
   return hipGetLastError();
 }
 
@@ -839,8 +684,7 @@ int64_t mk_max_batch(const DevFrame& fr) {
 hipError_t mk_render_staged(const DevScene& sc, const DevFrame& fr, int32_t stack_needed, void* ws,
                             size_t ws_bytes, float* accum, int32_t s_begin, int32_t s_count,
                             unsigned long long* counters, hipStream_t stream) {
-  const int64_t tiles = (int64_t)((fr.w + kMkTile - 1) / kMkTile) * ((fr.n_rows + kMkTile - 1) / kMkTile);
-  if (tiles >= PTMI_MK_DIRECT_MIN_TILES || s_count < 2)  // the tiles alone fill the chip: no staging
+  if (s_count < 2)  // one sample: direct accumulation, no staging
     return mk_render(sc, fr, stack_needed, accum, s_begin, s_count, counters, stream);
   const int32_t npix = fr.w * fr.n_rows;
   int32_t batch = s_count;

@@ -62,11 +62,6 @@ constexpr int kShards = 8;
                            // C3 +1.2 %, mesh fog +1.7 %; 64: C3 -6 %, mesh fog +2.3 %; profiles/r02/ab/ab_wf_block.log)
 #endif
 constexpr int kWfBlock = PTMI_WF_BLOCK;
-#ifndef PTMI_WF_EXACT_STACK
-// Leaf depth 16-18 (17-19 slots): kernels with exactly the slots needed
-// instead of the 20-slot ones (more blocks per CU fit the LDS stacks).
-#define PTMI_WF_EXACT_STACK 0
-#endif
 constexpr uint32_t kDead = 0xffffffffu;     // item of a retired slot
 constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (assigned in wf_intersect)
 
@@ -102,9 +97,6 @@ constexpr int32_t kMissRef = 0x7fffffff;
 // driven through its own intersect/shade/medium loop on its own stream, so
 // one pipe's kernels fill the drain at the end of the other's. They share the
 // work pool (next-unit counters) and the staging buffer.
-#ifndef PTMI_WF_DEFER_NOISE
-#define PTMI_WF_DEFER_NOISE 1
-#endif
 #ifndef PTMI_WF_PIPES
 #define PTMI_WF_PIPES 4  // A/B on MI355X: 1 -> 2 pipes +15 % (C3), 2 -> 4 +5 %
 #endif
@@ -153,15 +145,23 @@ __device__ __forceinline__ void wave_add(bool flag, int32_t* counter, int32_t si
 // loop; at kernel end the block sums through LDS and adds once. `scratch` may
 // alias LDS the kernel used before (the traversal stack): no extra LDS, which
 // would push a 32 KiB-stack block past 160 KiB / 5 and cost a wave per SIMD.
-__device__ __forceinline__ void block_flush(uint32_t v, void* scratch, unsigned long long* counter) {
+template <int N>
+__device__ __forceinline__ void block_flush(const uint32_t (&vals)[N], void* scratch, unsigned long long* counter) {
   unsigned int* lds = static_cast<unsigned int*>(scratch);
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  uint32_t v[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    v[k] = vals[k];
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) *lds = 0u;
+  if (threadIdx.x < N) lds[threadIdx.x] = 0u;
   __syncthreads();
-  if (lane_id() == 0 && v) atomicAdd(lds, v);
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    if (lane_id() == 0 && v[k]) atomicAdd(lds + k, v[k]);
   __syncthreads();
-  if (threadIdx.x == 0 && *lds) atomicAdd(counter, (unsigned long long)*lds);
+  if (threadIdx.x < N && lds[threadIdx.x]) atomicAdd(counter + threadIdx.x, (unsigned long long)lds[threadIdx.x]);
 }
 
 struct Ray {
@@ -170,42 +170,21 @@ struct Ray {
 };
 
 // Streamed buffers (queue records, hit records, medium lists, staging) go
-// through these helpers, with a cache-policy knob PTMI_WF_NT: 1 `nt` loads
-// and stores, 2 `nt` stores, 3 `sc1` stores (written line dropped from L2).
-// PMC: wf_intersect's L2 hit rate is 60 % against the megakernel's 96 %
-// (L1 hit rates 96 % / 98 %), the queue stream evicting BVH lines. But the
-// stage kernels re-read what the previous one wrote, and that reuse is worth
-// more: A/B on MI355X (parity-identical) C3 -10 % / -5 % / -5 %
+// through these helpers. PMC: wf_intersect's L2 hit rate is 60 % against the
+// megakernel's 96 % (L1 hit rates 96 % / 98 %), the queue stream evicting BVH
+// lines. But the stage kernels re-read what the previous one wrote, and that
+// reuse is worth more than streaming hints: A/B on MI355X (parity-identical),
+// `nt` loads + stores / `nt` stores / `sc1` stores, C3 -10 % / -5 % / -5 %
 // (profiles/r02/ab/ab_nontemporal.log, profiles/r02/pmc_cache/).
-#ifndef PTMI_WF_NT
-#define PTMI_WF_NT 0
-#endif
 typedef float pt_qf4 __attribute__((ext_vector_type(4)));
 typedef float pt_qf2 __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ __forceinline__ T s_load(const T* p) {
-#if PTMI_WF_NT == 1
-  return __builtin_nontemporal_load(p);
-#else
   return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void s_store(T* p, T v) {
-#if PTMI_WF_NT == 3
-  // s_nop: the store reads its data VGPRs after issue (VMEM store data
-  // hazard), which the compiler cannot see through inline asm
-  if constexpr (sizeof(T) == 16)
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-  else if constexpr (sizeof(T) == 8)
-    asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-  else
-    asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-#elif PTMI_WF_NT == 1 || PTMI_WF_NT == 2
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 __device__ __forceinline__ float4 q_load(const float4* p) {
   const pt_qf4 v = s_load((const pt_qf4*)p);
@@ -403,24 +382,34 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
     bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
     h_store(wb.hit + i, make_float2(t, __int_as_float(hit ? ref : kMissRef)));
   }
-  if (counters) block_flush(n_live, lds_stack, counters + 0);
+  if (counters) block_flush<1>({n_live}, lds_stack, counters + 0);
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
-// per-path wave budget of renderer.py:313.
+// per-path wave budget of renderer.py:313. A path it ends is counted in
+// ends[0] (Russian roulette) or ends[1] (depth or wave budget).
 __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scattered, pt_v3 hp, pt_v3 sdir, pt_v3 att,
-                                                 const Ray& cur, Rng& r, Ray& out) {
+                                                 const Ray& cur, Rng& r, Ray& out, uint32_t (&ends)[2]) {
   if (!scattered) return false;
   pt_v3 nthr = pt_mul(cur.thr, att);
   int32_t nd = (int32_t)(cur.meta & 0xffu) + 1;
-  if (nd >= fr.max_depth) return false;
+  if (nd >= fr.max_depth) {
+    ++ends[1];
+    return false;
+  }
   if (nd >= kRRMinDepth) {
     float sp = pt_minf(pt_maxf(pt_maxf(nthr.x, nthr.y), nthr.z), kRRMaxProb);
-    if (r.next() > sp) return false;
+    if (r.next() > sp) {
+      ++ends[0];
+      return false;
+    }
     nthr = pt_divs(nthr, sp);
   }
   int32_t wave = (int32_t)((cur.meta >> 8) & 0xffu);
-  if (wave + 1 >= fr.max_depth) return false;  // Q14: no wave left for the continuation
+  if (wave + 1 >= fr.max_depth) {  // Q14: no wave left for the continuation
+    ++ends[1];
+    return false;
+  }
   out.o = hp;
   out.d = sdir;
   out.thr = nthr;
@@ -449,7 +438,7 @@ __device__ __forceinline__ void finish_lane(const WfBufs& wb, int32_t i, bool en
 // `ray` whose closest hit (t, ref) has material g.
 __device__ __forceinline__ void shade_surface(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
                                               const Ray& ray, float t, int32_t ref, int32_t g, bool& ended,
-                                              bool& go, Ray& cont) {
+                                              bool& go, Ray& cont, uint32_t (&ends)[2]) {
   Item it = decode_item(fr, wb, ray.item);
   Rng r{path_key(fr, wb, it), ray.ctr};
   const Mat m = load_mat(sc, g);
@@ -460,7 +449,7 @@ __device__ __forceinline__ void shade_surface(const DevScene& sc, const DevFrame
   bool sc_ok;  // one unit-vector site for metal and isotropic lanes
   const int32_t ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, sc_ok);
   if (ruv != kRuvNone) sc_ok = scatter_end(sc, ruv, ref, m, hp, nrm, random_unit_vector(r), sdir, att);
-  go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont);
+  go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont, ends);
   if (!go) {
     ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
     stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
@@ -477,55 +466,11 @@ __device__ __forceinline__ bool noise_shaded(uint32_t flags) {
   return tx == 3u && (mt == 0u || mt == 4u);
 }
 
-#ifndef PTMI_WF_SORT
-#define PTMI_WF_SORT 0
-#endif
-constexpr int kWfWaves = kWfBlock / 64;
-
-// PTMI_WF_SORT: wf_shade writes the continuing rays of its 256-slot chunk back
-// sorted by direction octant (stable: slot order within an octant), into the
-// chunk's slots that held miss/surface rays, and marks the rest of those slots
-// as waiting for work; medium and deferred-noise slots stay where they are.
-// A ray record is self-contained (item, random-draw counter, depth and wave
-// count travel with it) and paths never interact, so which slot carries a
-// ray changes nothing in the results; the next wf_intersect's waves then hold
-// rays of one octant from nearby pixel squares. Block-uniform (two barriers).
-// A/B on MI355X (parity-identical): -8 % C3 and mesh fog: a wave's rays come
-// from one pixel square, and that origin coherence is worth more than the
-// direction coherence the sort buys (profiles/r02/ab/ab_wf_octant_sort.log).
-__device__ __forceinline__ void sorted_writeback(const Queue& q, int32_t i, bool ended, bool go, const Ray& cont,
-                                                 int32_t* sort_pos, int32_t (*sort_cnt)[8], int32_t* sort_nsurf) {
-  const int w = (int)(threadIdx.x >> 6);
-  const bool surf = ended || go;  // a miss / surface slot this pass rewrites
-  const int key = go ? ((cont.d.x < 0.0f ? 1 : 0) | (cont.d.y < 0.0f ? 2 : 0) | (cont.d.z < 0.0f ? 4 : 0)) : 0;
-  const unsigned long long ms = __ballot(surf);
-  unsigned long long mine = 0ull;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const unsigned long long m = __ballot(go && key == k);
-    if (lane_id() == 0) sort_cnt[w][k] = (int32_t)__popcll(m);
-    if (go && key == k) mine = m;
-  }
-  if (lane_id() == 0) sort_nsurf[w] = (int32_t)__popcll(ms);
-  __syncthreads();
-  int32_t soff = 0, n_go = 0, boff = 0;
-  for (int v = 0; v < kWfWaves; ++v) soff += v < w ? sort_nsurf[v] : 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-    for (int v = 0; v < kWfWaves; ++v) {
-      const int32_t c = sort_cnt[v][k];
-      n_go += c;
-      boff += (k < key || (k == key && v < w)) ? c : 0;
-    }
-  const int32_t srank = soff + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(ms >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ms, 0u));
-  if (surf) sort_pos[srank] = i;
-  __syncthreads();
-  if (go) {
-    const int32_t r = boff + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
-    store_ray(q, sort_pos[r], cont);
-  }
-  if (surf && srank >= n_go) s_store(reinterpret_cast<uint32_t*>(q.c + i) + 1, kPending);
-}
+// A/B, not kept: wf_shade writing its block's continuing rays back sorted by
+// direction octant (a ray record is self-contained, so its slot is free to
+// change): -8 % C3 and mesh fog. A wave's rays come from one pixel square, and
+// that origin coherence is worth more than the direction coherence the sort
+// buys (profiles/r02/ab/ab_wf_octant_sort.log).
 
 // shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
 // medium-boundary hits go to their shard's medium queue segment.
@@ -538,13 +483,8 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SHADE_MIN_WAVES) void wf_shade(De
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
-  __shared__ unsigned int tally;
-#if PTMI_WF_SORT
-  __shared__ int32_t sort_pos[kWfBlock];
-  __shared__ int32_t sort_cnt[kWfWaves][8];
-  __shared__ int32_t sort_nsurf[kWfWaves];
-#endif
-  uint32_t n_ended = 0;
+  __shared__ unsigned int tally[3];
+  uint32_t n_ended = 0, ends[2] = {0u, 0u};
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < wb.capacity; base += stride) {
     const int32_t i = base + (int32_t)threadIdx.x;
     bool to_medium = false, to_noise = false, ended = false, go = false;
@@ -562,29 +502,23 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SHADE_MIN_WAVES) void wf_shade(De
         const uint32_t fl = mat_flags(sc, g);
         if ((fl >> 8) & 1u) {
           to_medium = true;
-        } else if (PTMI_WF_DEFER_NOISE && noise_shaded(fl)) {
+        } else if (noise_shaded(fl)) {
           to_noise = true;
         } else {
-          shade_surface(sc, fr, wb, ray, h.x, ref, g, ended, go, cont);
+          shade_surface(sc, fr, wb, ray, h.x, ref, g, ended, go, cont, ends);
         }
       }
     }
     const int32_t mslot = wave_ticket(to_medium, ctl_medium(wb, shard));
     if (to_medium) s_store(wb.medq + shard * wb.medseg + mslot, i);
-#if PTMI_WF_DEFER_NOISE
     // deferred hits fill the shard's segment from the top; a slot is in at
     // most one of the two lists, so together they never exceed the segment
     const int32_t nslot = wave_ticket(to_noise, ctl_noise(wb, shard));
     if (to_noise) s_store(wb.medq + shard * wb.medseg + wb.medseg - 1 - nslot, i);
-#endif
-#if PTMI_WF_SORT
-    sorted_writeback(q, i, ended, go, cont, sort_pos, sort_cnt, sort_nsurf);
-#else
     finish_lane(wb, i, ended, go, cont);
-#endif
     n_ended += ended ? 1u : 0u;
   }
-  if (counters) block_flush(n_ended, &tally, counters + 2);
+  if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, tally, counters + 2);
 }
 
 // Constant-medium rays: exit traversal + free flight (apply_constant_medium,
@@ -607,22 +541,20 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
   int32_t nn = 0;  // deferred surface hits (wf_shade), after the medium rays in the index space
-#if PTMI_WF_DEFER_NOISE
   int32_t cntn[kShards];
 #pragma unroll
   for (int s = 0; s < kShards; ++s) {
     cntn[s] = __builtin_amdgcn_readfirstlane(*ctl_noise(wb, s));
     nn += cntn[s];
   }
-#endif
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
-  uint32_t n_ended = 0;
+  uint32_t n_ended = 0, ends[2] = {0u, 0u};
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
     Ray cont;
     int32_t i = -1, shard = 0;
-    const bool is_noise = PTMI_WF_DEFER_NOISE && j >= n && j < n + nn;
+    const bool is_noise = j >= n && j < n + nn;
     if (j < n) {  // medium-queue slot
       int32_t off = j;
 #pragma unroll
@@ -670,7 +602,9 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
         } else if (t_exit > 0.0f) {  // passthrough: same depth, next wave (kernels.py:1342-1350)
           passthrough = true;
           int32_t wave = (int32_t)((ray.meta >> 8) & 0xffu);
-          if (wave + 1 < fr.max_depth) {
+          if (wave + 1 >= fr.max_depth) {
+            ++ends[1];  // Q14: no wave left for the passthrough
+          } else {
             float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
             cont = ray;
             cont.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
@@ -693,7 +627,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
         if (ruv == kRuvMedium) sdir = v;
         else scattered = scatter_end(sc, ruv, ref, m, hp, nrm, v, sdir, att);
       }
-      if (!passthrough) go = scatter_epilogue(fr, scattered, hp, sdir, att, ray, r, cont);
+      if (!passthrough) go = scatter_epilogue(fr, scattered, hp, sdir, att, ray, r, cont, ends);
       if (!go) {
         ended = true;  // emissive surfaces add their emission once (:1368-1375); other ends add 0
         stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
@@ -703,7 +637,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
     finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
-  if (counters) block_flush(n_ended, lds_stack, counters + 2);
+  if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
 }
 
 namespace {
@@ -742,9 +676,6 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
 }
 #ifndef PTMI_WF_RB_CHUNK
 #define PTMI_WF_RB_CHUNK 8
-#endif
-#ifndef PTMI_WF_PIPELINED_RB
-#define PTMI_WF_PIPELINED_RB 1
 #endif
 #ifndef PTMI_WF_CAPACITY_LOG2
 #define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
@@ -788,9 +719,6 @@ static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must 
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs* wbs, float* accum, int32_t batch,
                            unsigned long long* counters, hipStream_t stream, const PipeStreams& ps) {
-#ifdef PTMI_WF_NOCOUNT
-  counters = nullptr;  // A/B only: prices the statistics atomics
-#endif
   // a pipe's grid = multiple of kShards and of the slot quantum, so its slot i
   // always maps to block (i / kWfBlock) % grid with shard (i / kWfBlock) % kShards
   int64_t blocks = wbs[0].capacity / kWfBlock;
@@ -819,14 +747,12 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
   int64_t it = 0;
   const int32_t chunk = PTMI_WF_RB_CHUNK;  // iterations between live-count readbacks
   hipError_t err = hipSuccess;
-#if PTMI_WF_PIPELINED_RB
   // The host reads chunk k's live counts only after chunk k + 1 is queued, so
   // the pipes never idle through the readback's host round trip. Iterations
   // on a drained pipe are no-ops (no slot holds or receives work), so the one
   // extra chunk a pipe may run after draining changes nothing.
   bool inflight[2][kPipes] = {};
   int cur = 0;
-#endif
   while (it < max_iters) {
     const int64_t n = max_iters - it < chunk ? max_iters - it : chunk;
     for (int64_t j = 0; j < n; ++j) {
@@ -846,7 +772,6 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     }
     it += n;
     err = hipGetLastError();
-#if PTMI_WF_PIPELINED_RB
     for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
       inflight[cur][p] = live[p];
       if (!live[p]) continue;
@@ -880,21 +805,6 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
         hipError_t e = hipEventSynchronize(ps.rb[k][p]);
         if (err == hipSuccess) err = e;
       }
-#else
-    for (int p = 0; p < kPipes && err == hipSuccess; ++p)
-      if (live[p])
-        err = hipMemcpyAsync(ps.pinned_live + p, ctl_live(wbs[p]), sizeof(int32_t), hipMemcpyDeviceToHost, st[p]);
-    for (int p = 0; p < kPipes && err == hipSuccess; ++p)
-      if (live[p]) err = hipStreamSynchronize(st[p]);
-    if (err != hipSuccess) break;
-    bool any = false;
-    for (int p = 0; p < kPipes; ++p) {
-      live[p] = live[p] && ps.pinned_live[p] != 0;
-      any = any || live[p];
-    }
-    if (!any) break;
-  }
-#endif
   for (int p = 1; p < kPipes; ++p) {  // join (also on error: the caller's stream must not run ahead)
     hipError_t e = hipEventRecord(ps.join[p], st[p]);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, ps.join[p], 0);
@@ -963,11 +873,6 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     hipError_t e;
     if (fr.traversal == PTMI_TRAV_STACKLESS) e = wf_batch<1, PTMI_TRAV_STACKLESS>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 16) e = wf_batch<16>(sc, fr, wbs, accum, nb, counters, stream, *ps);
-#if PTMI_WF_EXACT_STACK
-    else if (stack_needed == 17) e = wf_batch<17>(sc, fr, wbs, accum, nb, counters, stream, *ps);
-    else if (stack_needed == 18) e = wf_batch<18>(sc, fr, wbs, accum, nb, counters, stream, *ps);
-    else if (stack_needed == 19) e = wf_batch<19>(sc, fr, wbs, accum, nb, counters, stream, *ps);
-#endif
     else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wbs, accum, nb, counters, stream, *ps);

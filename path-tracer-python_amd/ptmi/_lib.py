@@ -11,9 +11,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PTMI_LIB') or os.path.join(_HERE, '_lib', 'libptmi.so')  # PTMI_LIB: A/B builds
-ABI_VERSION = 5  # PTMI_ABI_VERSION of include/ptmi.h
+ABI_VERSION = 6  # PTMI_ABI_VERSION of include/ptmi.h
 MAX_IMAGES = 16
-NUM_COUNTERS = 4
+NUM_COUNTERS = 5
 
 PTMI_OK, PTMI_EINVAL, PTMI_ECAPACITY, PTMI_EHIP, PTMI_ENODEV = 0, -1, -2, -3, -4
 
@@ -54,7 +54,7 @@ TRAVERSALS = {'stack': 0, 'stackless': 1}
 
 
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',
-           'ptmi_mk_render_ws', 'ptmi_mk_trace_ws', 'ptmi_mk_resolve_ws', 'ptmi_wf_workspace_bytes',
+           'ptmi_mk_render_ws', 'ptmi_mk_trace_ws', 'ptmi_mk_max_batch', 'ptmi_mk_resolve_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
            'ptmi_prof_stop', 'ptmi_prof_stop_busy', 'ptmi_node_bytes')
 PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_resolve', 'mk_resolve')
@@ -94,6 +94,8 @@ def load(path: str = LIB_PATH):
     lib.ptmi_mk_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_int32, C.c_int32, P, P]
     lib.ptmi_mk_workspace_bytes.argtypes = [C.POINTER(Frame), C.c_int32]
     lib.ptmi_mk_workspace_bytes.restype = C.c_size_t
+    lib.ptmi_mk_max_batch.argtypes = [C.POINTER(Frame)]
+    lib.ptmi_mk_max_batch.restype = C.c_int64
     lib.ptmi_mk_render_ws.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,
                                       C.c_int32, P, P]
     lib.ptmi_mk_trace_ws.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, C.c_int32, C.c_int32,

@@ -147,6 +147,7 @@ class Integrator:
             if with_counters else None
         self._ws = None
         self._ws_bytes = 0
+        self._reset_event = None  # counter reset the next overlapped trace must wait for
 
     def _cnt(self):
         return C.c_void_p(self.counters.data_ptr()) if self.counters is not None else None
@@ -198,23 +199,31 @@ class Integrator:
         are bit-identical to render_mk: the resolves add the same staged
         colours in the same sample order.
 
-        Ordering: a trace waits for the caller's stream as it was when the
-        *previous* overlapped call was made (that covers the resolve two
-        calls back, the last reader of its workspace) — not for later work,
-        which may include the previous trace's resolve. So the scene must not
-        change between overlapped calls, and work on the caller's stream
-        after this call sees the resolved accumulator as usual."""
+        Ordering, whatever stream each call passes:
+        * a trace into workspace half h waits for the resolve that last read
+          half h (an event recorded on the stream that ran that resolve), and
+          for a counter reset issued since the previous trace
+          (reset_counters records it);
+        * a resolve waits for its own trace and for the previous resolve, so
+          the accumulator sees the batches in call order;
+        * a trace does not wait for other work the caller queued after the
+          previous call: the scene must not change between overlapped calls,
+          and work on the caller's stream after this call sees the resolved
+          accumulator as usual."""
         import torch
         dev = self.scene.device
         caller = stream if stream is not None else torch.cuda.current_stream(dev)
         npix = frame.w * len(frame_pixel_rows(frame))
         if npix == 0 or sample_count <= 0:
             return
-        per = max(1, min(int(sample_count), self.STAGING_BYTES // max(1, 12 * npix)))
+        max_batch = int(self.lib.ptmi_mk_max_batch(C.byref(frame)))
+        if max_batch < 1:
+            _lib.check(-1, 'ptmi_mk_max_batch')
+        per = max(1, min(int(sample_count), self.STAGING_BYTES // max(1, 12 * npix), max_batch))
         with self._dev():
             if getattr(self, '_ov', None) is None:
                 self._ov = {'streams': [torch.cuda.Stream(dev), torch.cuda.Stream(dev)], 'ws': [None, None],
-                            'k': 0, 'prev_entry': None}
+                            'k': 0, 'resolved': [None, None], 'last_resolved': None}
             ov = self._ov
             b = 0
             while b < sample_count:
@@ -224,16 +233,20 @@ class Integrator:
                 need = int(self.lib.ptmi_mk_workspace_bytes(C.byref(frame), n))
                 if need == 0:
                     _lib.check(-1, 'ptmi_mk_workspace_bytes')
+                side = ov['streams'][h]
                 ws = ov['ws'][h]
                 if ws is None or ws.numel() * 4 < need:
                     torch.cuda.synchronize(dev)  # the old half may still be read by a trace or a resolve
                     ws = torch.empty((need + 15) // 16 * 4, dtype=torch.float32, device=dev)
                     ov['ws'][h] = ws
-                entry = torch.cuda.Event()
-                entry.record(caller)
-                side = ov['streams'][h]
-                side.wait_event(ov['prev_entry'] if ov['prev_entry'] is not None else entry)
-                ov['prev_entry'] = entry
+                    fresh = torch.cuda.Event()
+                    fresh.record(torch.cuda.current_stream(dev))  # the allocation's stream
+                    side.wait_event(fresh)
+                if ov['resolved'][h] is not None:
+                    side.wait_event(ov['resolved'][h])
+                if self._reset_event is not None:
+                    side.wait_event(self._reset_event)
+                    self._reset_event = None
                 _lib.check(self.lib.ptmi_mk_trace_ws(C.byref(self.scene.view), C.byref(frame),
                                                      C.c_void_p(ws.data_ptr()), ws.numel() * 4,
                                                      int(sample_begin) + b, n, self._cnt(),
@@ -241,9 +254,15 @@ class Integrator:
                 traced = torch.cuda.Event()
                 traced.record(side)
                 caller.wait_event(traced)
+                if ov['last_resolved'] is not None:
+                    caller.wait_event(ov['last_resolved'])
                 _lib.check(self.lib.ptmi_mk_resolve_ws(C.byref(frame), C.c_void_p(ws.data_ptr()), ws.numel() * 4,
                                                        C.c_void_p(accum.data_ptr()), n,
                                                        C.c_void_p(caller.cuda_stream)), 'ptmi_mk_resolve_ws')
+                done = torch.cuda.Event()
+                done.record(caller)
+                ov['resolved'][h] = done
+                ov['last_resolved'] = done
                 b += n
 
     def workspace(self, frame, sample_count=1, kind='wf'):
@@ -290,11 +309,17 @@ class Integrator:
         if self.counters is None:
             return None
         c = self.counters.cpu().numpy()
-        return {'segments': int(c[0]), 'medium': int(c[1]), 'paths': int(c[2])}
+        return {'segments': int(c[0]), 'medium': int(c[1]), 'paths': int(c[2]), 'rr': int(c[3]),
+                'depth_cap': int(c[4])}
 
-    def reset_counters(self):
+    def reset_counters(self, stream=None):
         if self.counters is not None:
-            self.counters.zero_()
+            s = stream if stream is not None else torch.cuda.current_stream(self.scene.device)
+            with torch.cuda.stream(s):
+                self.counters.zero_()
+            # overlapped traces run on side streams: the next one waits for this reset
+            self._reset_event = torch.cuda.Event()
+            self._reset_event.record(s)
 
 
 def _check_accum(accum, frame, device=None):

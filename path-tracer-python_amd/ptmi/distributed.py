@@ -29,6 +29,24 @@ class Shard:
     mode: str = 'samples'   # 'samples' | 'tiles'
     band_rows: int = 8
 
+    @classmethod
+    def balanced(cls, rank, world, mode, height, candidates=(8, 4, 2, 1), slack=0.01):
+        """Shard whose band height gives every rank a near-equal row count
+        (tiles): the tallest band among ``candidates`` whose largest rank
+        share is within ``slack`` of the smallest achievable one. 800 rows
+        over 8 ranks: 8-row bands give ranks 104 or 96 rows (100 bands, 4 %
+        over the even share), 4-row bands 100 each; 2160 rows: 8-row bands
+        (272 vs 270, kept). Taller bands keep more of a megakernel tile's 8
+        rows adjacent in the image."""
+        if mode != 'tiles' or world <= 1:
+            return cls(rank, world, mode)
+
+        def max_rows(b):
+            return max(len(cls(r, world, mode, b).rows(height)) for r in range(world))
+        best = min(max_rows(b) for b in candidates)
+        band = next(b for b in candidates if max_rows(b) <= best * (1 + slack))
+        return cls(rank, world, mode, band)
+
     def band(self):
         """(band_rows, band_stride, band_offset) for ptmi_frame."""
         if self.mode == 'tiles' and self.world > 1:

@@ -115,6 +115,7 @@ class MI355XRenderer:
 
     def _run(self, render_fn, label, resume=False):
         import torch
+        self._integrator_label = label
         self._upload_camera()
         spp = int(self.cam.samples_per_pixel)
         t0 = time.time()
@@ -164,8 +165,11 @@ class MI355XRenderer:
         self._run(self.integrator.render_wf, 'wavefront', resume)
 
     # ------------------------------------------------------- checkpoint/resume
-    # what must match for a checkpoint to continue this render exactly
-    _STATE_KEYS = ('seed', 'max_depth', 'background', 'traversal', 'width', 'height', 'camera', 'scene')
+    # what must match for a checkpoint to continue this render exactly; the
+    # integrator too: megakernel and wavefront paths differ (Q1, Q11, Q14), so
+    # a render resumed with the other one would match neither uninterrupted render
+    _STATE_KEYS = ('integrator', 'seed', 'max_depth', 'background', 'traversal', 'width', 'height', 'camera',
+                   'scene')
 
     def _render_state(self):
         import hashlib
@@ -176,17 +180,32 @@ class MI355XRenderer:
         f = self.frame
         cam = np.array([list(f.cam.center), list(f.cam.pixel00), list(f.cam.delta_u), list(f.cam.delta_v),
                         list(f.cam.defocus_u), list(f.cam.defocus_v), [f.cam.defocus_angle, 0.0, 0.0]], np.float32)
-        return {'seed': np.int64(f.seed), 'max_depth': np.int64(f.max_depth),
+        return {'integrator': np.array(getattr(self, '_integrator_label', '')), 'seed': np.int64(f.seed), 'max_depth': np.int64(f.max_depth),
                 'background': np.array(list(f.bg), np.float32), 'traversal': np.int64(f.traversal),
                 'width': np.int64(f.width), 'height': np.int64(f.height), 'camera': cam,
                 'scene': np.array(h.hexdigest())}
 
     def save_checkpoint(self, path):
-        """Write the accumulator and the next sample index (plain arrays, npz)."""
+        """Write the accumulator and the next sample index (plain arrays, npz)
+        to exactly ``path`` (no suffix added). The file is written next to it
+        under a temporary name and renamed over it, so a crash mid-save leaves
+        the previous checkpoint intact."""
+        import os
+        import tempfile
         import torch
         torch.cuda.synchronize(self.dscene.device)
         st = self._render_state()
-        np.savez(path, accum=self.accum.cpu().numpy(), next_sample=np.int64(self.current_sample), **st)
+        acc = self.accum.cpu().numpy()
+        d = os.path.dirname(os.path.abspath(path))
+        fd, tmp = tempfile.mkstemp(prefix='.ckpt-', suffix='.npz', dir=d)
+        try:
+            with os.fdopen(fd, 'wb') as f:
+                np.savez(f, accum=acc, next_sample=np.int64(self.current_sample), **st)
+            os.replace(tmp, path)
+        except BaseException:
+            if os.path.exists(tmp):
+                os.unlink(tmp)
+            raise
 
     def load_checkpoint(self, path):
         """Load a save_checkpoint() file into this renderer; render(resume=True)
@@ -196,6 +215,9 @@ class MI355XRenderer:
         render-time attributes have been applied."""
         import torch
         with np.load(path, allow_pickle=False) as z:
+            missing = [k for k in self._STATE_KEYS if k not in z.files]
+            if missing:
+                raise ValueError(f'{path} is not a checkpoint of this renderer version (missing {missing})')
             state = {k: z[k].copy() for k in self._STATE_KEYS}
             acc = z['accum'].copy()
             nxt = int(z['next_sample'])
@@ -226,6 +248,35 @@ class MI355XRenderer:
 
     _write_image = write_image
 
+    def _get_rr_stats(self):
+        """Russian-roulette statistics of the last render (renderer.py:481-500)
+        from the device counters: paths killed by RR (kernels.py:1145-1157), and
+        paths that reached the RR depth and survived to end another way (the
+        reference's rr_paths_survived). The reference's per-depth sums are not
+        kept (its atomics are disabled, kernels.py:1189-1202)."""
+        c = self.integrator.read_counters() or {}
+        killed = c.get('rr', 0)
+        return {'killed': killed, 'paths': c.get('paths', 0), 'depth_cap': c.get('depth_cap', 0),
+                'kill_rate': 100.0 * killed / c['paths'] if c.get('paths') else 0.0}
+
+    def _get_average_depth(self):
+        """Mean ray segments per path (renderer.py:473-479 reports the mean
+        depth-loop count; a segment is one traversal of that loop)."""
+        c = self.integrator.read_counters() or {}
+        return c['segments'] / c['paths'] if c.get('paths') else 0.0
+
+    def _print_depth_stats(self):
+        """Depth statistics block of renderer.py:502-523."""
+        c = self.integrator.read_counters() or {}
+        n = c.get('paths', 0)
+        if not n:
+            return
+        print('\nDepth Statistics:')
+        print(f'  Average path segments: {c["segments"] / n:.2f} (max depth: {self.max_depth})')
+        print(f'  Russian Roulette terminations: {c["rr"]:,} ({100.0 * c["rr"] / n:.1f}%)')
+        print(f'  Max depth terminations: {c["depth_cap"]:,} ({100.0 * c["depth_cap"] / n:.1f}%)')
+        print(f'  Total paths traced: {n:,}')
+
     def print_statistics(self):
         if not self.sample_times:
             return
@@ -239,8 +290,23 @@ class MI355XRenderer:
         if c.get('paths'):
             print(f'Segments/sample: {c["segments"] / c["paths"]:.3f} | '
                   f'medium traversals/sample: {c["medium"] / c["paths"]:.3f}')
+        self._print_depth_stats()
 
     _print_stats = print_statistics
+
+    # -------------------------------------------------- live preview (GUI, out of scope)
+    def setup_live_preview(self, update_interval_ms=500):
+        """renderer.py:593-616 opens a Tk window here. The Tk GUI is out of
+        scope (SURVEY.md §2), so this records the interval and opens nothing;
+        callers such as InteractiveViewer keep working headless."""
+        self.update_interval_ms = update_interval_ms
+        self.preview_window = None
+        self.last_preview_update = 0.0
+
+    def update_preview_if_needed(self):
+        """renderer.py:618-648: no window was opened (setup_live_preview), so
+        there is nothing to refresh; use image_u8() for the current image."""
+        return None
 
 
 TaichiRenderer = MI355XRenderer  # drop-in name (render_server.taichi_renderer.TaichiRenderer)

@@ -52,3 +52,34 @@ def test_algorithmic_bytes_cover_every_kernel_kind():
 def test_valu_diagnostic_for_the_default_workload():
     v = bench.valu_diagnostic(_args([]), 'megakernel')
     assert v is not None and 0 < v['valu_issue_frac'] <= 1 and 0 < v['lane_efficiency'] <= 1
+
+
+def test_multi_gpu_default_is_a_fixed_workload_tile_partition():
+    """--gpus N: interleaved row bands of the fixed total workload (strong
+    scaling, BASELINE.json configs[4]), total spp on the line."""
+    from ptmi.distributed import Shard
+    for preset, W, H, total in (('c2', 800, 800, 1024), ('c5', 3840, 2160, 4096)):
+        a = _args(['--preset', preset, '--gpus', '8'])
+        assert a.shard == 'tiles'
+        spp, scaling, cfg = bench.describe(a, W, H, 8, Shard.balanced(0, 8, a.shard, H))
+        assert spp == total == cfg['total_spp'] and scaling == 'strong'
+        assert cfg['partition'] == 'tiles' and cfg['parallelism'].startswith('tiles-shard x8')
+        assert f'@ {total} spp in total' in cfg['workload']
+    a = _args(['--gpus', '8', '--shard', 'samples'])
+    spp, scaling, _ = bench.describe(a, 800, 800, 8, Shard.balanced(0, 8, a.shard, 800))
+    assert spp == 8 * 1024 and scaling == 'weak'
+
+
+@pytest.mark.parametrize('H,world', [(800, 8), (800, 2), (800, 4), (2160, 8), (1024, 8), (225, 8), (7, 8)])
+def test_balanced_bands_cover_every_row_once(H, world):
+    import numpy as np
+    from ptmi.distributed import Shard
+    seen = np.zeros(H, np.int64)
+    sizes = []
+    for r in range(world):
+        rows = Shard.balanced(r, world, 'tiles', H).rows(H)
+        seen[rows] += 1
+        sizes.append(len(rows))
+    assert (seen == 1).all()
+    best = -(-H // world)
+    assert max(sizes) <= max(best * 1.01, best + 1) or H < world * 8

@@ -64,3 +64,59 @@ def test_two_rank_partition(tmp_path, mode):
         assert np.array_equal(got, ref, equal_nan=True)
     else:
         assert np.allclose(got / spp_total, ref / spp_total, rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
+def _bench_worker(rank, world, port, out_path):
+    """bench.py's multi-rank bookkeeping on gloo: the balanced tile partition,
+    the per-rank rows gathered to every rank (gather_ranks), the world size
+    the JSON line records; each rank's rows rendered by the oracle standing in
+    for its GPU, reduced onto rank 0."""
+    import json
+    import sys
+    for p in (ROOT, os.path.join(ROOT, 'path-tracer-python_amd'), os.path.join(ROOT, 'tests')):
+        sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import bench
+    from parity_helpers import oracle_render
+    from ptmi.distributed import Shard, reduce_accum
+    a = bench.parse(['--preset', 'c2', '--gpus', str(world), '--width', str(WIDTH), '--spp-per-step', str(SPS),
+                     '--steps', str(STEPS), '--dist-backend', 'gloo'])
+    H = WIDTH
+    sh = Shard.balanced(rank, world, a.shard, H)
+    acc = np.zeros((H, WIDTH, 3), np.float32)
+    rows = sh.rows(H)
+    for k in range(STEPS):
+        b, c = sh.sample_range(k, SPS)
+        for r in rows:
+            oracle_render(SCENE, WIDTH, 'mk', (0, r, WIDTH, 1), b, c, threads=1, acc=acc)
+    ranks = bench.gather_ranks([rank, len(rows)], 'cpu', world)
+    total_spp, scaling, cfg = bench.describe(a, WIDTH, H, world, sh)
+    t = torch.from_numpy(acc)
+    reduce_accum(t, dst=0)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+        with open(out_path + '.json', 'w') as f:
+            json.dump({'world_size': dist.get_world_size(), 'ranks': ranks, 'total_spp': total_spp,
+                       'scaling': scaling, 'config': cfg}, f)
+    dist.destroy_process_group()
+
+
+def test_bench_tile_partition_two_ranks(tmp_path):
+    import json
+    out = str(tmp_path / 'bench_tiles.npy')
+    mp.start_processes(_bench_worker, args=(2, _free_port(), out), nprocs=2, start_method='spawn')
+    with open(out + '.json') as f:
+        rec = json.load(f)
+    assert rec['world_size'] == 2 and [int(r[0]) for r in rec['ranks']] == [0, 1]
+    assert sum(int(r[1]) for r in rec['ranks']) == WIDTH  # every row on exactly one rank
+    assert rec['config']['partition'] == 'tiles' and rec['scaling'] == 'strong'
+    assert rec['total_spp'] == SPS * STEPS
+    ref, _ = oracle_render_full()
+    assert np.array_equal(np.load(out), ref, equal_nan=True)  # bit-identical to one device
+
+
+def oracle_render_full():
+    from parity_helpers import oracle_render
+    return oracle_render(SCENE, WIDTH, 'mk', (0, 0, WIDTH, WIDTH), 0, SPS * STEPS)

@@ -1,0 +1,177 @@
+"""GPU parity at the benchmark's own call shapes.
+
+The window tests (test_gpu_parity.py) render small frames from sample 0 with
+1-8 spp per call. bench.py's timed region runs differently: whole frames,
+64 (C2, C3), 32 (C4) or 16 (C5) samples per call at sample indices in the
+hundreds or thousands, through the persistent staged megakernel with
+overlapped launches (two traces in flight, 8 unit shards with stealing), or
+the 4-pipe wavefront. These tests drive bench.BenchRun — the object bench.py
+times — exactly as bench.py does and compare the result against the CPU
+oracle (oracle/, test infrastructure only):
+
+* three consecutive calls from sample 1536 on: scattered 64x64 windows of the
+  full frame against the oracle over the same samples (bit-exact expected);
+* one call from sample 1536 on over the WHOLE frame: every pixel, and the
+  device's segment / medium / path / Russian-roulette / depth-budget counters
+  against the oracle's (the same paths, segment for segment);
+* bench.py's exact default sequence (2 warm-up steps, accumulator cleared,
+  16 timed steps: samples 128-1151, the north star's 1024 spp) on two
+  windows at full spp;
+* the 8-GPU tile partition (bench.py --gpus 8: each rank renders its
+  interleaved row bands) run rank by rank on this GPU: the bands together are
+  bit-identical to the 1-GPU frame.
+
+Tolerance: per-pixel L-inf of accum/spp <= 1e-4 (north star), >= 99.9 % of
+pixels bit-identical; measured: 0 and 100 %.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from parity_helpers import compare
+
+pytestmark = pytest.mark.gpu
+
+LINF_TOL = 1e-4
+S0 = 1536  # first sample of the checked calls
+THREADS = min(16, os.cpu_count() or 1)
+
+_runs = {}
+
+
+def bench_run(preset, extra=()):
+    import torch
+    import bench
+    key = (preset, tuple(extra))
+    if key not in _runs:
+        a = bench.parse(['--preset', preset, *extra])
+        _runs[key] = bench.BenchRun(a, torch.device('cuda', 0))
+    return _runs[key]
+
+
+def oracle_windows(run, windows, s_begin, s_count):
+    import oracle
+    a = run.a
+    acc = np.zeros((run.H, run.W, 3), np.float32)
+    osc = oracle.OracleScene(run.sa)
+    fr = oracle.make_frame(run.cam, run.bg, a.max_depth, a.seed, run.W, run.H, a.traversal)
+    st = {}
+    for win in windows:
+        s = oracle.render(osc, fr, a.variant, acc, win, s_begin, s_count, THREADS)
+        for k, v in s.items():
+            st[k] = st.get(k, 0) + v
+    return acc, st
+
+
+def windows_of(run, n=5, size=64, seed=7):
+    """Deterministic scattered windows: the centre plus n-1 random ones."""
+    W, H = run.W, run.H
+    rng = np.random.default_rng(seed)
+    wins = [((W - size) // 2, (H - size) // 2, size, size)]
+    while len(wins) < n:
+        x, y = int(rng.integers(0, W - size + 1)), int(rng.integers(0, H - size + 1))
+        wins.append((x, y, size, size))
+    return wins
+
+
+def steps_of(run, ncalls):
+    k0 = S0 // run.sps
+    assert run.sample_base(k0) == S0
+    return list(range(k0, k0 + ncalls))
+
+
+def check_windows(g, o, windows, spp, what):
+    for (x0, y0, w, h) in windows:
+        linf, exact = compare(g[y0:y0 + h, x0:x0 + w], o[y0:y0 + h, x0:x0 + w], spp)
+        print(f'{what} window {(x0, y0, w, h)}: L-inf={linf:.3g} identical={exact:.5f}')
+        assert linf <= LINF_TOL
+        assert exact >= 0.999
+
+
+@pytest.mark.parametrize('preset', ['c2', 'c3', 'c4', 'c5'])
+def test_three_consecutive_bench_calls_match_oracle(preset):
+    import torch
+    run = bench_run(preset)
+    acc = torch.zeros((run.H, run.W, 3), dtype=torch.float32, device='cuda')
+    steps = steps_of(run, 3)
+    for k in steps:
+        run.step(acc, k)
+    torch.cuda.synchronize()
+    g = acc.cpu().numpy()
+    assert np.isfinite(g).all() and g.any()
+    wins = windows_of(run, 5 if preset != 'c5' else 6)
+    o, _ = oracle_windows(run, wins, S0, 3 * run.sps)
+    check_windows(g, o, wins, 3 * run.sps, f'{preset} calls {steps}')
+
+
+@pytest.mark.parametrize('preset', ['c2', 'c3', 'c4', 'c5'])
+def test_one_bench_call_full_frame_and_counters(preset):
+    """One bench call (sample 1536 on) over the whole frame: every pixel and
+    every device counter against the oracle."""
+    import torch
+    run = bench_run(preset)
+    acc = torch.zeros((run.H, run.W, 3), dtype=torch.float32, device='cuda')
+    torch.cuda.synchronize()
+    run.integ.reset_counters()
+    run.step(acc, steps_of(run, 1)[0])
+    torch.cuda.synchronize()
+    g = acc.cpu().numpy()
+    gst = run.integ.read_counters()
+    o, ost = oracle_windows(run, [(0, 0, run.W, run.H)], S0, run.sps)
+    linf, exact = compare(g, o, run.sps)
+    print(f'{preset} full frame {run.W}x{run.H} x {run.sps} spp from {S0}: L-inf={linf:.3g} '
+          f'identical={exact:.6f} gpu={gst} oracle={ost}')
+    assert linf <= LINF_TOL and exact >= 0.999
+    assert gst == ost  # segments, medium exits, paths, RR kills, depth-budget ends
+    assert gst['paths'] == run.W * run.H * run.sps
+
+
+@pytest.mark.parametrize('preset', ['c2', 'c3'])
+def test_bench_timed_region_at_full_spp(preset):
+    """bench.py's default sequence at the north star's 1024 spp: warm-up
+    steps, accumulator cleared, the timed steps; two windows at full spp."""
+    import torch
+    import bench
+    run = bench_run(preset)
+    a = bench.parse(['--preset', preset])
+    acc = torch.zeros((run.H, run.W, 3), dtype=torch.float32, device='cuda')
+    for k in range(a.warmup):
+        run.step(acc, k)
+    torch.cuda.synchronize()
+    acc.zero_()
+    for k in range(a.steps):
+        run.step(acc, a.warmup + k)
+    torch.cuda.synchronize()
+    g = acc.cpu().numpy()
+    spp = a.steps * run.sps
+    assert spp == 1024
+    wins = windows_of(run, 2, seed=11)
+    o, _ = oracle_windows(run, wins, run.sample_base(a.warmup), spp)
+    check_windows(g, o, wins, spp, f'{preset} timed region {a.warmup}..{a.warmup + a.steps - 1}')
+
+
+@pytest.mark.parametrize('preset', ['c2', 'c5'])
+def test_eight_rank_tile_partition_is_bit_identical(preset):
+    """bench.py --gpus 8 (tiles): each rank's bands, rendered here one rank
+    after the other with the bench's call shape, add up to the 1-GPU frame."""
+    import torch
+    from ptmi import device
+    from ptmi.distributed import Shard
+    run = bench_run(preset)
+    k = steps_of(run, 1)[0]
+    full = torch.zeros((run.H, run.W, 3), dtype=torch.float32, device='cuda')
+    run.step(full, k)
+    parts = torch.zeros_like(full)
+    a = run.a
+    rows_seen = np.zeros(run.H, np.int64)
+    for r in range(8):
+        sh = Shard.balanced(r, 8, 'tiles', run.H)
+        rows_seen[sh.rows(run.H)] += 1
+        fr = device.make_frame(run.cam, run.bg, a.max_depth, a.seed, run.W, run.H, band=sh.band(),
+                               traversal=a.traversal)
+        run.integ.render_mk(fr, parts, run.sample_base(k), run.sps, overlap=True) if a.variant == 'mk' else \
+            run.integ.render_wf(fr, parts, run.sample_base(k), run.sps)
+    torch.cuda.synchronize()
+    assert (rows_seen == 1).all()  # every row rendered by exactly one rank
+    assert torch.equal(parts, full)

@@ -35,5 +35,6 @@ def test_full_frame_parity(case):
     assert linf <= LINF_TOL
     assert exact >= 0.999
     assert gst['paths'] == W * H * spp == ost['paths']
-    # same paths, segment for segment: the device's traversal counters equal the oracle's
-    assert gst['segments'] == ost['segments'] and gst['medium'] == ost['medium']
+    # same paths, segment for segment: the device's traversal, Russian-roulette
+    # and depth-budget counters equal the oracle's
+    assert gst == ost

@@ -156,3 +156,60 @@ def test_prof_busy_time_is_the_union_of_overlapping_launches():
             torch.cuda.synchronize()
     mk2 = kt2.result['megakernel']
     assert abs(mk2['busy_ms'] - mk2['ms']) <= 1e-3 * max(1.0, mk2['ms'])
+
+
+def test_mk_overlapped_batches_respect_the_item_id_limit():
+    """render_mk(overlap=True) splits a call into batches that fit one
+    ptmi_mk_trace_ws (ptmi_mk_max_batch), like the staged path above."""
+    import ctypes as C
+    import torch
+    from edge_scenes import edge_scene
+    from ptmi import device
+    sa, cam, bg = edge_scene('empty')
+    W, H = cam['width'], cam['height']
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, W, H, (0, 0, 1, 1))
+    mb = integ.lib.ptmi_mk_max_batch(C.byref(fr))
+    assert mb == ((1 << 32) - 1) // (8 * 64)  # one tile, padded to the 8 unit shards
+    n = 3 * mb + 5
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
+    integ.reset_counters()
+    integ.render_mk(fr, acc, 0, n, overlap=True)
+    torch.cuda.synchronize()
+    assert integ.read_counters()['paths'] == n
+    want = np.add.accumulate(np.full(n, np.float32(bg[0]), np.float32))[-1]
+    assert acc[0, 0, 0].item() == want
+
+
+def test_mk_overlapped_calls_on_changing_streams():
+    """Overlapped calls whose caller stream changes from call to call, with a
+    counter reset between calls and no synchronisation: the accumulator and
+    the counters equal the plain same-stream calls bit for bit (each trace
+    waits for the last resolve that read its workspace half and for the
+    reset; each resolve for the previous resolve)."""
+    import torch
+    from ptmi import device
+    sa, cam, bg = scene_inputs('vol2_final_scene', 800)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, cam['width'], cam['height'], (128, 256, 320, 192))
+    calls = [(0, 5), (5, 3), (8, 6), (14, 2), (16, 4), (20, 3)]
+    ref = torch.zeros((cam['height'], cam['width'], 3), dtype=torch.float32, device='cuda')
+    for s0, n in calls[:2]:
+        integ.render_mk(fr, ref, s0, n)
+    integ.reset_counters()
+    for s0, n in calls[2:]:
+        integ.render_mk(fr, ref, s0, n)
+    torch.cuda.synchronize()
+    want_cnt = integ.read_counters()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.current_stream()]
+    acc = torch.zeros_like(ref)
+    torch.cuda.synchronize()
+    for j, (s0, n) in enumerate(calls):
+        if j == 2:
+            integ.reset_counters(stream=streams[j % 3])
+        integ.render_mk(fr, acc, s0, n, stream=streams[j % 3], overlap=True)
+    for s in streams:
+        s.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(acc, ref)
+    assert integ.read_counters() == want_cnt

@@ -45,6 +45,7 @@ def test_parity(case, variant):
     mask[y0:y0 + h, x0:x0 + w] = False
     assert not np.any(g[mask])
     assert gst['paths'] == w * h * spp == ost['paths']
+    assert gst == ost  # segments, medium exits, Russian-roulette and depth-budget ends too
 
 
 @pytest.mark.parametrize('variant', ['mk', 'wf'])

@@ -156,3 +156,50 @@ def test_periodic_checkpoints_during_render(tmp_path):
     r.render()
     with np.load(r.checkpoint_path, allow_pickle=False) as z:
         assert int(z['next_sample']) == 4  # the last chunk boundary before the end
+
+
+def test_checkpoint_refuses_the_other_integrator(tmp_path):
+    """A megakernel checkpoint cannot be resumed by render_wavefront (the two
+    integrators draw different samples: Q1, Q11, Q14), nor the reverse."""
+    part = _smoke_renderer(2, str(tmp_path / 'part.png'))
+    part.render()
+    ck = str(tmp_path / 'mk.ckpt')  # no .npz suffix: saved and loaded under exactly this name
+    part.save_checkpoint(ck)
+    assert os.path.exists(ck) and not os.path.exists(ck + '.npz')
+    other = _smoke_renderer(4, str(tmp_path / 'other.png'))
+    other.load_checkpoint(ck)
+    with pytest.raises(ValueError, match='integrator'):
+        other.render_wavefront(resume=True)
+    wf = _smoke_renderer(2, str(tmp_path / 'wf.png'))
+    wf.render_wavefront()
+    wf.save_checkpoint(ck)  # replaces the file atomically
+    mk = _smoke_renderer(4, str(tmp_path / 'mk.png'))
+    mk.load_checkpoint(ck)
+    with pytest.raises(ValueError, match='integrator'):
+        mk.render(resume=True)
+    mk.load_checkpoint(ck)
+    mk.render_wavefront(resume=True)  # the same integrator resumes
+    assert mk.current_sample == 4
+    assert not [f for f in os.listdir(tmp_path) if f.startswith('.ckpt-')]  # no temporary left behind
+
+
+def test_rr_statistics_match_the_oracle(tmp_path):
+    """print_statistics' Russian-roulette / depth-budget figures
+    (renderer.py:481-523) are the device counters, equal to the oracle's."""
+    from parity_helpers import oracle_render
+    from ptmi import scenes
+    from ptmi.renderer import TaichiRenderer
+    random.seed(1234)
+    sc = scenes.wavefront_comparison()
+    sc.cam.img_width = 400
+    sc.cam.samples_per_pixel = 4
+    r = TaichiRenderer(sc.world, sc.cam, str(tmp_path / 'rr.png'))
+    r.background_color = sc.background
+    r.max_depth = sc.max_depth
+    r.render()
+    st = r._get_rr_stats()
+    _, ost = oracle_render('wavefront_comparison', 400, 'mk', (0, 0, 400, 225), 0, 4)
+    assert st['killed'] == ost['rr'] > 0 and st['depth_cap'] == ost['depth_cap']
+    assert st['paths'] == ost['paths'] == 400 * 225 * 4
+    r.setup_live_preview(250)  # GUI hooks: headless no-ops
+    assert r.update_preview_if_needed() is None
