@@ -188,6 +188,16 @@ class Integrator:
 
     # staging budget for the per-(sample, pixel) colour slots of one batch
     STAGING_BYTES = 1 << 30
+    # Overlapped megakernel calls: traces in flight, one workspace and side
+    # stream each. Two for full-frame calls; three for small calls, whose
+    # drain is a larger part of a launch. A/B on MI355X (vol2 800x800, 64 spp
+    # per call): the full frame (41 M samples per call) 2851 (2) vs 2762 (3)
+    # Msamples/s; an 8-GPU tile shard (5.1 M samples per call, rehearsed on one
+    # GPU, tools/shard_balance.py) 2380-2487 (2) vs 2450-2565 (3) per GPU; 4
+    # in flight is slower than both (profiles/r03/overlap_depth_and_bands.log).
+    # PTMI_OVERLAP_DEPTH fixes the depth (A/B only).
+    OVERLAP_DEPTH_MAX = 3
+    OVERLAP_SMALL_CALL = 8_000_000  # samples per call below which 3 traces overlap
 
     def render_mk_overlapped(self, frame, accum, sample_begin, sample_count, stream=None):
         """Megakernel calls whose launches overlap: each batch is traced
@@ -203,7 +213,9 @@ class Integrator:
         * a trace into workspace half h waits for the resolve that last read
           half h (an event recorded on the stream that ran that resolve), and
           for a counter reset issued since the previous trace
-          (reset_counters records it);
+          (reset_counters records it; the reset and read_counters in turn
+          wait for the traces still adding to the counters, whatever stream
+          they run on);
         * a resolve waits for its own trace and for the previous resolve, so
           the accumulator sees the batches in call order;
         * a trace does not wait for other work the caller queued after the
@@ -222,13 +234,17 @@ class Integrator:
         per = max(1, min(int(sample_count), self.STAGING_BYTES // max(1, 12 * npix), max_batch))
         with self._dev():
             if getattr(self, '_ov', None) is None:
-                self._ov = {'streams': [torch.cuda.Stream(dev), torch.cuda.Stream(dev)], 'ws': [None, None],
-                            'k': 0, 'resolved': [None, None], 'last_resolved': None}
+                D = self.OVERLAP_DEPTH_MAX
+                self._ov = {'streams': [torch.cuda.Stream(dev) for _ in range(D)], 'ws': [None] * D,
+                            'k': 0, 'resolved': [None] * D, 'last_resolved': None, 'traced': [None] * D}
             ov = self._ov
+            depth = int(os.environ.get('PTMI_OVERLAP_DEPTH', '0')) or \
+                (3 if npix * min(per, int(sample_count)) < self.OVERLAP_SMALL_CALL else 2)
+            depth = max(1, min(depth, len(ov['ws'])))
             b = 0
             while b < sample_count:
                 n = min(per, int(sample_count) - b)
-                h = ov['k'] % 2
+                h = ov['k'] % depth  # any rotation is safe: each half waits for its own last reader
                 ov['k'] += 1
                 need = int(self.lib.ptmi_mk_workspace_bytes(C.byref(frame), n))
                 if need == 0:
@@ -253,6 +269,7 @@ class Integrator:
                                                      C.c_void_p(side.cuda_stream)), 'ptmi_mk_trace_ws')
                 traced = torch.cuda.Event()
                 traced.record(side)
+                ov['traced'][h] = traced
                 caller.wait_event(traced)
                 if ov['last_resolved'] is not None:
                     caller.wait_event(ov['last_resolved'])
@@ -305,9 +322,19 @@ class Integrator:
                                              int(spp), self._stream(stream)), 'ptmi_tonemap')
         return out
 
+    def _after_traces(self, stream):
+        """Make `stream` wait for the overlapped traces in flight: they add to
+        the counters from their side streams."""
+        ov = getattr(self, '_ov', None)
+        if ov is not None:
+            for ev in ov['traced']:
+                if ev is not None:
+                    stream.wait_event(ev)
+
     def read_counters(self):
         if self.counters is None:
             return None
+        self._after_traces(torch.cuda.current_stream(self.scene.device))
         c = self.counters.cpu().numpy()
         return {'segments': int(c[0]), 'medium': int(c[1]), 'paths': int(c[2]), 'rr': int(c[3]),
                 'depth_cap': int(c[4])}
@@ -315,6 +342,7 @@ class Integrator:
     def reset_counters(self, stream=None):
         if self.counters is not None:
             s = stream if stream is not None else torch.cuda.current_stream(self.scene.device)
+            self._after_traces(s)
             with torch.cuda.stream(s):
                 self.counters.zero_()
             # overlapped traces run on side streams: the next one waits for this reset

@@ -1,22 +1,47 @@
 #!/usr/bin/env python3
-"""Statistical golden: the reference's own path tracer on a Lambertian scene.
+"""Statistical goldens: the reference's own path tracer on small scenes.
 
 TEST INFRASTRUCTURE ONLY (run in the build container, where /root/reference
 exists; never at test time, never on the GPU box). It imports the reference's
 pure-Python integrator read-only — core/camera.py `get_ray` + `ray_color`
-(camera.py:74-137), core/material.py lambertian, util/vec3.py
-random_cosine_direction — renders a small all-Lambertian scene (spheres over a
-ground sphere, constant sky) and saves the per-pixel mean and variance of the
-sample colours (float64) to stat_lambert.npz, plus the scene in
-stat_lambert.json. SURVEY.md §8c item (6).
+(camera.py:74-137), core/material.py, core/quad.py, core/texture.py,
+core/constant_medium.py, util/vec3.py — renders each scene below at SPP
+samples per pixel and saves the per-pixel mean and variance of the sample
+colours (float64) to stat_<scene>.npz, plus the scene in stat_<scene>.json.
+SURVEY.md §8c item (6). Usage: gen_statistical.py [scene ...] (default: all).
 
-Why this pins the oracle: for Lambertian spheres seen from outside under a
-constant sky, the Taichi kernels' semantics (kernels.py) and the Python
-integrator differ only in ways that keep the expectation: RR (both unbiased;
-disabled here on the Python side), the cosine-sampling basis (Q4, same
-distribution), the depth cap (Q13; albedo <= 0.8 makes bounces beyond 49
-negligible) and the RNG. tests/test_statistical.py compares the oracle's
-per-pixel means against these, within the standard errors of both.
+Why this pins the oracle: on these scenes the Taichi kernels' semantics
+(kernels.py) and the Python integrator differ only in ways that keep the
+expectation: RR (both unbiased; disabled here on the Python side), the
+cosine-sampling basis (Q4, same distribution), the extra dielectric draw
+(Q28), the depth cap (Q13; albedo <= 0.8 makes bounces beyond 49 negligible)
+and the RNG. tests/test_statistical.py compares the oracle's per-pixel means
+against these, within the standard errors of both.
+
+  * lambert    — Lambertian spheres under a constant sky;
+  * materials  — glass, mirror (fuzz 0) and Lambertian spheres lit by an
+                 emissive sphere;
+  * quads      — an open box of Lambertian quads (normals face-flipped toward
+                 the ray in both integrators, quad.py:61 / Q2) lit by an
+                 emissive quad (emission from both sides in both, Q6), a
+                 checker-textured sphere (floor-mod parity, texture.py:47-56 /
+                 Q9) and an image-textured sphere (the earthmap, sphere UV +
+                 v flip, sphere.py:72-82, texture.py:66-79 / Q8, Q30), seen
+                 through a defocus camera (camera.py:64-67, 128-131);
+  * medium     — an isolated constant-medium sphere (nothing inside it)
+                 against the sky and an emissive sphere. The two integrators
+                 agree on the first free-flight segment only: entry at the
+                 boundary, exit at the boundary's far side (kernels.py:417-419
+                 finds it as the closest hit beyond the entry), free flight
+                 -1/density * log(u) (constant_medium.py:31-58 / Q10, Q24).
+                 After a scatter inside, the kernels treat the far wall as a
+                 new entry with no exit and shade it as a surface (Q10), the
+                 Python medium samples again: different transport. So the
+                 Python side runs at max_depth 1 (a scattered path adds
+                 nothing) and the kernels at max_depth 2 (the passthrough
+                 consumes one wave / loop iteration, Q11, Q14; a path that
+                 scattered ends at the wall's fallback shading with 0): both
+                 then measure exactly transmittance x what lies behind.
 """
 import json
 import multiprocessing as mp
@@ -30,6 +55,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 SCENES = {
+    # Each scene: camera, background, max_depth (the Python integrator's;
+    # 'kernel_max_depth' for the oracle when different), and objects:
+    # spheres [center, radius, material], quads [Q, u, v, material], media
+    # [boundary sphere center, radius, density, albedo]. Materials:
+    # ['lambertian', rgb], ['checker', scale, rgb even, rgb odd],
+    # ['image', 'earthmap.jpg'], ['diffuse_light', rgb], ['dielectric', ir],
+    # ['metal', rgb] (fuzz 0).
     # all-Lambertian spheres under a constant sky
     'lambert': {
         'width': 32, 'aspect': 16.0 / 9.0, 'vfov': 30.0, 'lookfrom': [0.0, 0.6, 3.0], 'lookat': [0.0, 0.1, -1.0],
@@ -54,25 +86,83 @@ SCENES = {
             [[0.0, -0.05, -1.4], 0.45, ['lambertian', [0.2, 0.3, 0.7]]],
         ],
     },
+    # open quad box lit by a quad light, checker + earthmap spheres, defocus camera
+    'quads': {
+        'width': 32, 'aspect': 16.0 / 9.0, 'vfov': 40.0, 'lookfrom': [0.0, 1.0, 4.2], 'lookat': [0.0, 0.9, 0.0],
+        'vup': [0.0, 1.0, 0.0], 'background': [0.0, 0.0, 0.0], 'max_depth': 50,
+        'defocus_angle': 1.5, 'focus_distance': 4.0,
+        'spheres': [
+            [[-0.6, 0.45, -0.2], 0.45, ['checker', 0.2, [0.1, 0.25, 0.1], [0.8, 0.8, 0.75]]],
+            [[0.65, 0.5, 0.1], 0.5, ['image', 'earthmap.jpg']],
+        ],
+        'quads': [  # Q, u, v, material
+            [[-2.0, 0.0, -1.5], [4.0, 0.0, 0.0], [0.0, 0.0, 3.5], ['lambertian', [0.7, 0.7, 0.7]]],   # floor
+            [[-2.0, 0.0, -1.5], [0.0, 2.4, 0.0], [4.0, 0.0, 0.0], ['lambertian', [0.6, 0.6, 0.65]]],  # back
+            [[-2.0, 0.0, -1.5], [0.0, 0.0, 3.5], [0.0, 2.4, 0.0], ['lambertian', [0.65, 0.1, 0.1]]],  # left
+            [[2.0, 0.0, -1.5], [0.0, 2.4, 0.0], [0.0, 0.0, 3.5], ['lambertian', [0.12, 0.5, 0.15]]],  # right
+            [[-2.0, 2.4, -1.5], [4.0, 0.0, 0.0], [0.0, 0.0, 3.5], ['lambertian', [0.7, 0.7, 0.7]]],   # ceiling
+            [[-0.6, 2.38, -0.7], [1.2, 0.0, 0.0], [0.0, 0.0, 1.0], ['diffuse_light', [6.0, 6.0, 6.0]]],  # light
+        ],
+    },
+    # isolated constant-medium sphere against the sky and an emissive sphere
+    'medium': {
+        'width': 32, 'aspect': 16.0 / 9.0, 'vfov': 34.0, 'lookfrom': [0.0, 0.3, 4.0], 'lookat': [0.0, 0.0, 0.0],
+        'vup': [0.0, 1.0, 0.0], 'background': [0.7, 0.8, 1.0], 'max_depth': 1, 'kernel_max_depth': 2,
+        'spheres': [
+            [[0.9, 0.3, -2.0], 0.8, ['diffuse_light', [2.0, 1.2, 0.4]]],
+        ],
+        'media': [  # boundary sphere center, radius, density, albedo
+            [[-0.2, 0.0, 0.0], 0.9, 0.9, [0.8, 0.8, 0.8]],
+        ],
+    },
 }
 SPP = 4096
 NAME = 'lambert'
+
+
+REF_IMAGES = '/root/reference/src/assets/images'
+
+
+def _material(spec):
+    from core.material import dielectric, diffuse_light, lambertian, metal  # noqa: E402
+    from core.texture import checker_texture, image_texture  # noqa: E402
+    from util import color  # noqa: E402
+    kind, p = spec[0], spec[1:]
+    if kind == 'lambertian':
+        return lambertian.from_color(color(*p[0]))
+    if kind == 'checker':
+        return lambertian.from_texture(checker_texture.from_colors(p[0], color(*p[1]), color(*p[2])))
+    if kind == 'image':
+        return lambertian.from_texture(image_texture(os.path.join(REF_IMAGES, p[0])))
+    if kind == 'diffuse_light':
+        return diffuse_light.from_color(color(*p[0]))
+    if kind == 'dielectric':
+        return dielectric(p[0])
+    if kind == 'metal':
+        return metal(color(*p[0]), 0.0)
+    raise ValueError(kind)
 
 
 def _build():
     from gen_fixtures import _install_stubs
     _install_stubs()
     from core import Sphere, hittable_list, camera  # noqa: E402
-    from core.material import dielectric, diffuse_light, lambertian, metal  # noqa: E402
+    from core.constant_medium import constant_medium  # noqa: E402
+    from core.material import lambertian  # noqa: E402
+    from core.quad import quad  # noqa: E402
     from util import color, point3, vec3  # noqa: E402
     SCENE = SCENES[NAME]
     world = hittable_list()
-    for c, r, (kind, p) in SCENE['spheres']:
-        mat = {'lambertian': lambda: lambertian.from_color(color(*p)),
-               'diffuse_light': lambda: diffuse_light.from_color(color(*p)),
-               'dielectric': lambda: dielectric(p), 'metal': lambda: metal(color(*p), 0.0)}[kind]()
-        world.add(Sphere.stationary(point3(*c), r, mat))
+    for c, r, spec in SCENE.get('spheres', []):
+        world.add(Sphere.stationary(point3(*c), r, _material(spec)))
+    for q, u, v, spec in SCENE.get('quads', []):
+        world.add(quad(point3(*q), vec3(*u), vec3(*v), _material(spec)))
+    for c, r, density, albedo in SCENE.get('media', []):
+        boundary = Sphere.stationary(point3(*c), r, lambertian.from_color(color(0.5, 0.5, 0.5)))
+        world.add(constant_medium.from_color(boundary, color(*albedo), density))
     cam = camera()
+    cam.defocus_angle = SCENE.get('defocus_angle', 0.0)
+    cam.focus_distance = SCENE.get('focus_distance', 10.0)
     cam.aspect_ratio = SCENE['aspect']
     cam.img_width = SCENE['width']
     cam.samples_per_pixel = SPP
@@ -109,7 +199,7 @@ def _rows(args):
 
 def main():
     global NAME
-    for NAME in SCENES:
+    for NAME in (sys.argv[1:] or SCENES):
         render_one()
 
 
