@@ -46,8 +46,11 @@ enum {
  *             ref >= 0: internal node, as its BYTE offset in nodes
  *             (index x 80: the traversal adds it to the node base with
  *             no index scaling); ref < 0: leaf code
- *             0x80000000 | type << 28 | prim index (type: 0 sphere,
- *             1 triangle, 2 quad — scene_compiler.py:10-12).
+ *             0x80000000 | type << 28 | class << 25 | prim index (type: 0
+ *             sphere, 1 triangle, 2 quad — scene_compiler.py:10-12; class:
+ *             the primitive's PTMI_CLASS_* from its material flags, used by
+ *             the wavefront to sort hits by material without a load;
+ *             prim index < 2^25 per type). ABI v6.
  *   spheres : ns x 4 f32 {cx, cy, cz, r}                (fields.py:25)
  *   quads   : nq x 16 f32 {n.xyz, D | Q.xyz, u.x | u.yz, v.xy | v.z, w.xyz}
  *   tris    : nt x 12 f32 {v0.xyz, e1.x | e1.yz, e2.xy | e2.z, n.xyz}
@@ -124,6 +127,17 @@ typedef struct ptmi_frame {
  * fields.py:287). Accumulated with atomics; pass NULL to skip. [3] and [4]
  * since ABI v6 (the buffer must hold PTMI_NUM_COUNTERS entries). */
 #define PTMI_NUM_COUNTERS 5
+
+/* Material class in a leaf code (bits 25-27), from the material flags:
+ * constant-medium boundary; Perlin-textured Lambertian or isotropic; else by
+ * material type: Lambertian 0, dielectric 2, emissive 3, glossy otherwise
+ * (metal 1, isotropic 4, unknown types). */
+#define PTMI_CLASS_LAMBERTIAN 0
+#define PTMI_CLASS_GLOSSY 1
+#define PTMI_CLASS_DIELECTRIC 2
+#define PTMI_CLASS_MEDIUM 3
+#define PTMI_CLASS_NOISE 4
+#define PTMI_CLASS_EMISSIVE 5
 
 int ptmi_version(void);
 const char *ptmi_last_error(void);

@@ -73,6 +73,8 @@ static int to_dev_scene(const ptmi_scene_view* s, DevScene& d) {
   if (s->num_spheres < 0 || s->num_quads < 0 || s->num_triangles < 0 || s->n_inner < 0)
     return fail(PTMI_EINVAL, "negative scene counts");
   if (np > 0x0fffffff) return fail(PTMI_ECAPACITY, "too many primitives (%d)", np);
+  if (s->num_spheres > (1 << 25) || s->num_quads > (1 << 25) || s->num_triangles > (1 << 25))
+    return fail(PTMI_ECAPACITY, "more than 2^25 primitives of one type (25-bit leaf index)");
   if (np > 0 && s->n_inner != np - 1)
     return fail(PTMI_EINVAL, "binary BVH with one primitive per leaf needs n_inner = prims - 1 (%d vs %d)",
                 s->n_inner, np - 1);

@@ -21,6 +21,20 @@ constexpr float kTMax = 1e10f;
 constexpr int kRRMinDepth = 5;      // kernels.py:1050
 constexpr float kRRMaxProb = 0.95f; // kernels.py:1051
 constexpr int kNumCounters = PTMI_NUM_COUNTERS;  // include/ptmi.h
+
+// n / d by one 64-bit multiply and shift: m = floor(2^(32+l) / d) + 1 with
+// 2^l >= d gives floor(n / d) exactly whenever n * d < 2^(32+l), which every
+// use below guarantees (work-item and unit ids < 2^32, divisors <= 2^l).
+struct FastDiv {
+  uint64_t m;
+  uint32_t sh, d;
+};
+static inline FastDiv fast_div(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  return FastDiv{((1ull << (32 + l)) / d) + 1ull, 32u + l, d};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (uint32_t)(((uint64_t)n * f.m) >> f.sh); }
 constexpr int kBlock = 256;
 
 enum : int32_t { kSphere = 0, kTriangle = 1, kQuad = 2 };
@@ -58,7 +72,9 @@ struct DevFrame {
 };
 
 __device__ __forceinline__ int32_t leaf_type(int32_t ref) { return (ref >> 28) & 3; }
-__device__ __forceinline__ int32_t leaf_index(int32_t ref) { return ref & 0x0fffffff; }
+__device__ __forceinline__ int32_t leaf_index(int32_t ref) { return ref & 0x01ffffff; }
+// material class of a leaf (PTMI_CLASS_*, include/ptmi.h), packed by the host
+__device__ __forceinline__ int32_t leaf_class(int32_t ref) { return (ref >> 25) & 7; }
 
 // Local row (0..n_rows-1) -> image row, or -1.
 __device__ __forceinline__ int32_t frame_row(const DevFrame& fr, int32_t lr) {
@@ -727,6 +743,20 @@ __device__ __forceinline__ float reflectance(float c, float ri) {  // kernels.py
   return r0 + (1.0f - r0) * pt_pow5f(1.0f - c);
 }
 
+// Dielectric scatter direction, kernels.py:876-903 (attenuation 1).
+__device__ __forceinline__ pt_v3 scatter_dielectric(const Mat& m, pt_v3 dir, pt_v3 n, Rng& r) {
+  float ir = m.m1.w;
+  bool front = pt_dot(dir, n) < 0.0f;
+  pt_v3 nf = front ? n : pt_neg(n);
+  float ratio = front ? (1.0f / ir) : ir;
+  pt_v3 ud = pt_normalize(dir);
+  float ct = pt_minf(-pt_dot(ud, nf), 1.0f);
+  float st = sqrtf(1.0f - ct * ct);
+  bool cannot = ratio * st > 1.0f;
+  float u = r.next();  // unconditional draw
+  return (cannot || reflectance(ct, ratio) > u) ? reflect3(ud, nf) : refract3(ud, nf, ratio);
+}
+
 // scatter(), kernels.py:818-917. Returns scattered; writes direction and
 // attenuation. Material record already loaded.
 __device__ __forceinline__ bool scatter(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 dir, pt_v3 hp,
@@ -749,16 +779,7 @@ __device__ __forceinline__ bool scatter(const DevScene& sc, int32_t ref, const M
     return false;
   }
   if (mt == 2) {
-    float ir = m.m1.w;
-    bool front = pt_dot(dir, n) < 0.0f;
-    pt_v3 nf = front ? n : pt_neg(n);
-    float ratio = front ? (1.0f / ir) : ir;
-    pt_v3 ud = pt_normalize(dir);
-    float ct = pt_minf(-pt_dot(ud, nf), 1.0f);
-    float st = sqrtf(1.0f - ct * ct);
-    bool cannot = ratio * st > 1.0f;
-    float u = r.next();  // unconditional draw
-    sdir = (cannot || reflectance(ct, ratio) > u) ? reflect3(ud, nf) : refract3(ud, nf, ratio);
+    sdir = scatter_dielectric(m, dir, n, r);
     return true;
   }
   if (mt == 4) {
@@ -798,16 +819,7 @@ __device__ __forceinline__ int32_t scatter_begin(const DevScene& sc, int32_t ref
     return kRuvMetal;
   }
   if (mt == 2) {
-    float ir = m.m1.w;
-    bool front = pt_dot(dir, n) < 0.0f;
-    pt_v3 nf = front ? n : pt_neg(n);
-    float ratio = front ? (1.0f / ir) : ir;
-    pt_v3 ud = pt_normalize(dir);
-    float ct = pt_minf(-pt_dot(ud, nf), 1.0f);
-    float st = sqrtf(1.0f - ct * ct);
-    bool cannot = ratio * st > 1.0f;
-    float u = r.next();  // unconditional draw
-    sdir = (cannot || reflectance(ct, ratio) > u) ? reflect3(ud, nf) : refract3(ud, nf, ratio);
+    sdir = scatter_dielectric(m, dir, n, r);
     scattered = true;
     return kRuvNone;
   }

@@ -136,18 +136,6 @@ constexpr int kMkBlock = 64;
                             // (re-tuned: 2 is +3 % on C2 but -8 % on C4's long fog paths;
                             // profiles/r01/ab_fetch_sizing.log)
 #endif
-// n / d for n < 2^26 by one 64-bit multiply: m = floor(2^(32+l) / d) + 1 with
-// 2^l >= d is exact because n * d < 2^(32+l) (items < 2^32, so units < 2^26).
-struct FastDiv {
-  uint64_t m;
-  uint32_t sh, d;
-};
-static inline FastDiv fast_div(uint32_t d) {
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  return FastDiv{((1ull << (32 + l)) / d) + 1ull, 32u + l, d};
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (uint32_t)(((uint64_t)n * f.m) >> f.sh); }
 
 // Unit counters: the units are split into PTMI_MK_SHARDS contiguous shards,
 // each with its own counter on its own 256-B line, and wave w pulls from shard

@@ -4,13 +4,23 @@
 // TaichiRenderer.render_wavefront (renderer.py:305-334). Stages and layout
 // are designed for CDNA4, not translated:
 //   * ray queue = three float4 streams per slot (A = o.xyz,d.x;
-//     B = d.yz,thr.xy; C = thr.z, work item, rng draw counter, meta) so every
-//     load/store is a 16-B-per-lane coalesced access; meta = depth | wave << 8;
+//     B = d.yz, work item, rng draw counter; C = thr.xyz, meta) so every
+//     load/store is a 16-B-per-lane coalesced access; meta = depth | wave << 8.
+//     wf_intersect reads A and B only: the ray and its slot state in 32 B;
 //   * hit record = 8 B (t, leaf ref); hit point and normal are recomputed in
 //     the shading kernel with the reference's own expressions;
-//   * rays whose closest hit is a constant-medium boundary are compacted into
-//     a separate medium queue and get their exit traversal (kernels.py:417)
-//     from a dedicated kernel instead of diverging inside shading;
+//   * CLOSEST-HIT CLASSIFICATION: wf_intersect ends the paths a hit or miss
+//     ends without a scatter (miss: shade_miss_rays, kernels.py:1266-1280;
+//     emissive: kernels.py:1365-1375) and compacts every other slot, by its
+//     hit's material, into one of five lists with wave64 ballot + mbcnt (one
+//     atomic per wave and list): Lambertian, metal/isotropic, dielectric,
+//     constant-medium boundary, Perlin-textured surface;
+//   * PER-MATERIAL SHADE KERNELS: wf_shade_lambertian / wf_shade_glossy /
+//     wf_shade_dielectric each run one material's scatter (kernels.py:817-917)
+//     over their list, so a wave executes one material's code only;
+//     wf_medium does the constant-medium exit traversal (kernels.py:417) and
+//     free flight, and the Perlin-textured surfaces (three octaves of table
+//     gathers, kernels.py:1013-1015) after them;
 //   * WORK POOL, IN-PLACE SLOTS: the reference pushes one sample of every
 //     pixel through max_depth bounce-synchronous waves (renderer.py:305-334)
 //     and compacts survivors into a next queue with one atomic per ray, so
@@ -28,8 +38,9 @@
 //     device-wide counter saturates near 88 returning atomics/us on MI355X
 //     (MI355X_MICROARCH.md, "dequeue") and was measured at 97 % wait cycles.
 //   * PIPES: the queue is split into 4 independent parts, each looping
-//     intersect -> shade -> medium on its own stream, so the drain at the end
-//     of one pipe's launch is filled by another's (+21 % over one pipe).
+//     intersect -> shade (3 material kernels) -> medium on its own stream, so
+//     the drain at the end of one pipe's launch is filled by another's (+21 %
+//     over one pipe).
 //   * The host learns that a pipe has drained from a 4-byte live count read
 //     back every 8 iterations, and waits for chunk k's counts only after
 //     chunk k + 1 is queued, so no pipe idles through the host round trip
@@ -67,14 +78,21 @@ constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (
 
 struct Queue {
   float4* a;  // o.xyz, d.x
-  float4* b;  // d.y, d.z, thr.x, thr.y
-  float4* c;  // thr.z, item, rng counter, meta (bits)
+  float4* b;  // d.y, d.z, item (bits), rng counter (bits)
+  float4* c;  // thr.xyz, meta (bits)
 };
+
+// Closest-hit lists (wf_intersect fills them, the shading kernels drain them).
+// Each list holds kShards segments of medseg slot indices; the medium and
+// Perlin lists share one array, the Perlin one filling its segments from the top
+// (a slot is in at most one list, so together they never exceed a segment).
+enum : int32_t { kListLambertian = 0, kListGlossy = 1, kListDielectric = 2, kListMedium = 3, kListNoise = 4,
+                 kLists = 5 };
 
 struct WfBufs {
   Queue q;
   float2* hit;        // t, ref (bits); ref kMissRef = miss
-  int32_t* medq;      // kShards segments of medseg slot indices
+  int32_t* lists;     // 4 arrays of capacity indices: Lambertian, glossy, dielectric, medium + Perlin
   float* staging;     // [batch][npix][3] path colours
   int32_t* ctl;       // this pipe's counters, one per 256-B line (see ctl_*)
   int32_t* next;      // next-unit counters shared by the pipes, one per 256-B line
@@ -89,6 +107,7 @@ struct WfBufs {
   int32_t shard_len;  // units per shard (a multiple of csamp): shard s owns [s*len, min((s+1)*len, nunits))
   int32_t shard_groups; // 64-slot groups drawing from each shard
   int32_t s_begin;    // first sample of the batch
+  FastDiv by_per, by_nsq, by_sqx;  // item decode: / (64 * csamp), / nsq, / sq_x
 };
 
 constexpr int32_t kMissRef = 0x7fffffff;
@@ -104,17 +123,25 @@ constexpr int32_t kPipes = PTMI_WF_PIPES;
 
 // Device-scope atomics are performed per cache line at the memory side, so
 // counters sharing a line serialize as one: every counter gets its own
-// 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 17 lines:
-// medium-queue count per shard, live slots (read by the host), deferred-
-// shading count per shard.
+// 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 81
+// lines: live slots (read by the host), and two sets (by iteration parity)
+// of one count per list and shard. wf_intersect of iteration k appends to set
+// k & 1 and the shading kernels read it; wf_medium, the iteration's last
+// kernel, zeroes set (k + 1) & 1 for the next iteration's wf_intersect.
 constexpr int32_t kLine = 64;
-constexpr int32_t kPipeLines = 17;
+constexpr int32_t kPipeLines = 1 + 2 * kLists * 8;
 constexpr int32_t kCtlWords = (8 + kPipeLines * kPipes) * kLine;
-__host__ __device__ __forceinline__ int32_t* ctl_medium(const WfBufs& wb, int32_t s) { return wb.ctl + s * kLine; }
 __host__ __device__ __forceinline__ int32_t* ctl_next(const WfBufs& wb, int32_t s) { return wb.next + s * kLine; }
-__host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl + 8 * kLine; }
-// deferred-shading (Perlin-textured surface hits) count per shard: lines 9-16
-__host__ __device__ __forceinline__ int32_t* ctl_noise(const WfBufs& wb, int32_t s) { return wb.ctl + (9 + s) * kLine; }
+__host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl; }
+__host__ __device__ __forceinline__ int32_t* ctl_list(const WfBufs& wb, int32_t par, int32_t list, int32_t s) {
+  return wb.ctl + (1 + (par * kLists + list) * 8 + s) * kLine;
+}
+// slot-index entry k of shard s's segment of a list
+__device__ __forceinline__ int32_t* list_slot(const WfBufs& wb, int32_t list, int32_t s, int32_t k) {
+  const int32_t arr = list < kListMedium ? list : 3;
+  int32_t* seg = wb.lists + (size_t)arr * (size_t)wb.capacity + (size_t)s * (size_t)wb.medseg;
+  return list == kListNoise ? seg + wb.medseg - 1 - k : seg + k;
+}
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -197,18 +224,20 @@ __device__ __forceinline__ float2 h_load(const float2* p) {
 }
 __device__ __forceinline__ void h_store(float2* p, float2 v) { s_store((pt_qf2*)p, pt_qf2{v.x, v.y}); }
 
-__device__ __forceinline__ void store_ray(const Queue& q, int32_t i, const Ray& r) {
-  q_store(q.a + i, make_float4(r.o.x, r.o.y, r.o.z, r.d.x));
-  q_store(q.b + i, make_float4(r.d.y, r.d.z, r.thr.x, r.thr.y));
-  q_store(q.c + i, make_float4(r.thr.z, __uint_as_float(r.item), __uint_as_float(r.ctr), __uint_as_float(r.meta)));
+__device__ __forceinline__ void store_ray_v(const Queue& q, int32_t i, pt_v3 o, pt_v3 d, pt_v3 thr, uint32_t item,
+                                            uint32_t ctr, uint32_t meta) {
+  s_store((pt_qf4*)(q.a + i), pt_qf4{o.x, o.y, o.z, d.x});
+  s_store((pt_qf4*)(q.b + i), pt_qf4{d.y, d.z, __uint_as_float(item), __uint_as_float(ctr)});
+  s_store((pt_qf4*)(q.c + i), pt_qf4{thr.x, thr.y, thr.z, __uint_as_float(meta)});
 }
 
-__device__ __forceinline__ void kill_slot(const Queue& q, int32_t i) {
-  s_store(reinterpret_cast<uint32_t*>(q.c + i) + 1, kDead);
+// The slot's state lives in its work-item word (B.z): an item, kPending or kDead.
+__device__ __forceinline__ void set_slot_item(const Queue& q, int32_t i, uint32_t v) {
+  s_store(reinterpret_cast<uint32_t*>(q.b + i) + 2, v);
 }
 
 __device__ __forceinline__ uint32_t slot_item(const Queue& q, int32_t i) {
-  return s_load(reinterpret_cast<const uint32_t*>(q.c + i) + 1);
+  return s_load(reinterpret_cast<const uint32_t*>(q.b + i) + 2);
 }
 
 __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
@@ -216,9 +245,9 @@ __device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
   Ray r;
   r.o = pt_v3f(a.x, a.y, a.z);
   r.d = pt_v3f(a.w, b.x, b.y);
-  r.thr = pt_v3f(b.z, b.w, c.x);
-  r.item = __float_as_uint(c.y);
-  r.ctr = __float_as_uint(c.z);
+  r.item = __float_as_uint(b.z);
+  r.ctr = __float_as_uint(b.w);
+  r.thr = pt_v3f(c.x, c.y, c.z);
   r.meta = __float_as_uint(c.w);
   return r;
 }
@@ -236,10 +265,11 @@ struct Item {
 };
 __device__ __forceinline__ Item decode_item(const DevFrame& fr, const WfBufs& wb, uint32_t k) {
   Item it;
+  // multiply-shift divisions (exact: items < 2^31, FastDiv)
   const uint32_t per = 64u * (uint32_t)wb.csamp;
-  const uint32_t c = k / per, j = k - c * per;
-  const uint32_t blk = c / (uint32_t)wb.nsq, q = c - blk * (uint32_t)wb.nsq;
-  const int32_t qy = (int32_t)(q / (uint32_t)wb.sq_x), qx = (int32_t)q - qy * wb.sq_x;
+  const uint32_t c = fdiv(k, wb.by_per), j = k - c * per;
+  const uint32_t blk = fdiv(c, wb.by_nsq), q = c - blk * (uint32_t)wb.nsq;
+  const int32_t qy = (int32_t)fdiv(q, wb.by_sqx), qx = (int32_t)q - qy * wb.sq_x;
   const int32_t lx = qx * 8 + (int32_t)(j & 7u), lr = qy * 8 + (int32_t)((j >> 3) & 7u);
   it.srel = (int32_t)blk * wb.csamp + (int32_t)(j >> 6);
   it.valid = lx < fr.w && lr < fr.n_rows && it.srel < wb.batch;
@@ -253,18 +283,6 @@ __device__ __forceinline__ uint32_t path_key(const DevFrame& fr, const WfBufs& w
   return pt_path_key(fr.seed, (uint32_t)(it.py * fr.width + it.px), (uint32_t)(wb.s_begin + it.srel));
 }
 
-// generate_camera_rays, kernels.py:1219-1239 (direction left unnormalized, Q1).
-__device__ __forceinline__ Ray camera_ray(const DevFrame& fr, const WfBufs& wb, uint32_t k) {
-  Item it = decode_item(fr, wb, k);
-  Rng rng{path_key(fr, wb, it), 0u};
-  Ray r;
-  get_ray(fr, it.px, it.py, rng, r.o, r.d);
-  r.thr = pt_v3f(1.0f, 1.0f, 1.0f);
-  r.item = k;
-  r.ctr = rng.n;
-  r.meta = 0u;
-  return r;
-}
 
 __device__ __forceinline__ void stage(const DevFrame& fr, const WfBufs& wb, uint32_t k, pt_v3 c) {
   const Item it = decode_item(fr, wb, k);
@@ -301,7 +319,7 @@ __device__ __forceinline__ int2 fetch_units(const WfBufs& wb, int32_t shard) {
 // starts at its first unit.
 __global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb, int32_t init_next) {
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kWfBlock)) {
-    reinterpret_cast<uint32_t*>(wb.q.c + i)[1] = kPending;
+    reinterpret_cast<uint32_t*>(wb.q.b + i)[2] = kPending;
     if ((i & 63) == 0) wb.grp[i >> 6] = make_int2(0, 0);
   }
   if (init_next && blockIdx.x < kShards && threadIdx.x == 0) {
@@ -313,11 +331,14 @@ __global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb, 
 
 // Hand the group's (this wave's) next items to its slots waiting for work,
 // taking a new chunk when the current one runs out; slots that find no work
-// retire. Wave-uniform: called by all 64 lanes of the group.
-__device__ __forceinline__ void assign_work(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& item) {
+// retire. Wave-uniform: called by all 64 lanes of the group. A slot given a
+// camera ray gets its origin and direction in (o, d) too (true returned; its
+// throughput is 1), so the caller need not read back what was just stored.
+__device__ __forceinline__ bool assign_work(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& item,
+                                            pt_v3& o, pt_v3& d) {
   const bool pending = item == kPending;
   const unsigned long long pm = __ballot(pending);
-  if (pm == 0ull) return;
+  if (pm == 0ull) return false;
   const int32_t g = i >> 6;
   const uint32_t n = (uint32_t)__popcll(pm);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
@@ -344,52 +365,141 @@ __device__ __forceinline__ void assign_work(const DevFrame& fr, const WfBufs& wb
     nxt += n;
   }
   if (lane_id() == 0) wb.grp[g] = make_int2((int32_t)nxt, (int32_t)end);
+  bool fresh = false;
   if (pending) {
     if (my == kDead) {
-      kill_slot(wb.q, i);
+      set_slot_item(wb.q, i, kDead);
       item = kDead;
     } else if (decode_item(fr, wb, my).valid) {
-      store_ray(wb.q, i, camera_ray(fr, wb, my));
+      // generate_camera_rays, kernels.py:1219-1239 (direction left unnormalized, Q1)
+      const Item it = decode_item(fr, wb, my);
+      Rng rng{path_key(fr, wb, it), 0u};
+      get_ray(fr, it.px, it.py, rng, o, d);
+      store_ray_v(wb.q, i, o, d, pt_v3f(1.0f, 1.0f, 1.0f), my, rng.n, 0u);
       item = my;
+      fresh = true;
     }  // an item outside the frame / batch: the slot stays pending
   }
   wave_add(pending && my == kDead, ctl_live(wb), -1);
+  return fresh;
 }
 
-// intersect_rays, kernels.py:1242-1263.
+// Path end without a scatter (a miss, or an emissive / absorbing hit): its
+// one colour (or 0) to the staging slot, and the slot waits for work.
+__device__ __forceinline__ void end_path(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t item, pt_v3 c) {
+  stage(fr, wb, item, c);
+  set_slot_item(wb.q, i, kPending);
+}
+
+// Closest-hit classes (PTMI_CLASS_*, include/ptmi.h) are packed into the
+// leaf codes by the host, so a hit's list is known without a material load.
+// Surface hits whose scatter evaluates Perlin turbulence (a noise texture on
+// a Lambertian or isotropic material, kernels.py:1013-1015) have their own
+// class, shaded by wf_medium: a marble lane would otherwise put three octaves
+// of table round trips into every Lambertian wave that holds it.
+static_assert(PTMI_CLASS_LAMBERTIAN == kListLambertian && PTMI_CLASS_GLOSSY == kListGlossy &&
+                  PTMI_CLASS_DIELECTRIC == kListDielectric && PTMI_CLASS_MEDIUM == kListMedium &&
+                  PTMI_CLASS_NOISE == kListNoise,
+              "leaf classes are list ids");
+
+// intersect_rays, kernels.py:1242-1263, plus the closest-hit classification:
+// shade_miss_rays (kernels.py:1266-1280) and emissive hits end their paths
+// here; every other traced slot is appended to its material's list.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-__global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid};
-  if (blockIdx.x < kShards && tid == 0) {  // medium and deferred-shading counts of this iteration
-    *ctl_medium(wb, blockIdx.x) = 0;
-    *ctl_noise(wb, blockIdx.x) = 0;
-  }
   const Queue q = wb.q;
+  const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
+  const int32_t shard = (int32_t)(blockIdx.x % kShards);
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
-  uint32_t n_live = 0;
+  uint32_t n_live = 0, n_ended = 0;
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + tid); i < wb.capacity; i += stride) {
-    uint32_t item = slot_item(q, i);
-    assign_work(fr, wb, i, item);  // generate_camera_rays (kernels.py:1219-1239) for slots that need work
-    if (item >= kPending) continue;
-    ++n_live;
-    float4 a = q_load(q.a + i), b = q_load(q.b + i);
-    pt_v3 o = pt_v3f(a.x, a.y, a.z), d = pt_v3f(a.w, b.x, b.y);
-    float t;
-    int32_t ref;
-    bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
-    h_store(wb.hit + i, make_float2(t, __int_as_float(hit ? ref : kMissRef)));
+    const float4 b = q_load(q.b + i);
+    uint32_t item = __float_as_uint(b.z);
+    pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
+    // generate_camera_rays (kernels.py:1219-1239) for slots that need work
+    const bool fresh = assign_work(fr, wb, i, item, o, d);
+    int32_t list = -1;
+    if (item < kPending) {
+      ++n_live;
+      if (!fresh) {
+        const float4 a = q_load(q.a + i);
+        o = pt_v3f(a.x, a.y, a.z);
+        d = pt_v3f(a.w, b.x, b.y);
+      }
+      float t;
+      int32_t ref;
+      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
+      if (hit) {
+        list = leaf_class(ref);
+        h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
+      }
+      if (!hit || list == PTMI_CLASS_EMISSIVE) {
+        // a miss (thr * bg) or an emissive hit (thr * emit, if any), then the path ends
+        pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);  // a fresh camera ray's
+        if (!fresh) {
+          const float4 c = q_load(q.c + i);
+          thr = pt_v3f(c.x, c.y, c.z);
+        }
+        pt_v3 col = pt_mul(thr, bg);
+        if (hit) {
+          const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
+          col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z))
+                                                         : pt_v3f(0.0f, 0.0f, 0.0f);
+        }
+        end_path(fr, wb, i, item, col);
+        ++n_ended;
+        list = -1;
+      }
+    }
+    // wave-uniform appends, one atomic per wave and non-empty list; lane 0
+    // issues them all before it waits for any (independent round trips)
+    unsigned long long m[kLists];
+    int32_t got[kLists];
+#pragma unroll
+    for (int32_t l = 0; l < kLists; ++l) {
+      m[l] = pt_ballot(list == l);
+      got[l] = 0;
+    }
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int32_t l = 0; l < kLists; ++l)
+        if (m[l]) got[l] = atomicAdd(ctl_list(wb, par, l, shard), (int32_t)__popcll(m[l]));
+    }
+    // broadcast lane 0's bases: in converged code (every lane of the wave
+    // active here), so that lane 0 takes part whatever its own list
+    int32_t b0 = 0;
+    unsigned long long ml = 0ull;
+#pragma unroll
+    for (int32_t l = 0; l < kLists; ++l) {
+      const int32_t bl = __shfl(got[l], 0);
+      if (list == l) {
+        b0 = bl;
+        ml = m[l];
+      }
+    }
+    if (list >= 0) {
+      const int32_t k = b0 + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
+      if (k < wb.medseg) s_store(list_slot(wb, list, shard, k), i);  // always true: a shard has medseg slots
+    }
   }
-  if (counters) block_flush<1>({n_live}, lds_stack, counters + 0);
+  if (counters) {
+    block_flush<1>({n_live}, lds_stack, counters + 0);
+    block_flush<1>({n_ended}, lds_stack, counters + 2);
+  }
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
-// per-path wave budget of renderer.py:313. A path it ends is counted in
-// ends[0] (Russian roulette) or ends[1] (depth or wave budget).
-__device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scattered, pt_v3 hp, pt_v3 sdir, pt_v3 att,
-                                                 const Ray& cur, Rng& r, Ray& out, uint32_t (&ends)[2]) {
+// per-path wave budget of renderer.py:313: a continuing ray is stored back
+// into its slot i (true returned). A path it ends is counted in ends[0]
+// (Russian roulette) or ends[1] (depth or wave budget).
+__device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, const WfBufs& wb, int32_t i, bool scattered,
+                                                 pt_v3 hp, pt_v3 sdir, pt_v3 att, const Ray& cur, Rng& r,
+                                                 uint32_t (&ends)[2]) {
   if (!scattered) return false;
   pt_v3 nthr = pt_mul(cur.thr, att);
   int32_t nd = (int32_t)(cur.meta & 0xffu) + 1;
@@ -410,172 +520,136 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scatte
     ++ends[1];
     return false;
   }
-  out.o = hp;
-  out.d = sdir;
-  out.thr = nthr;
-  out.item = cur.item;
-  out.ctr = r.n;
-  out.meta = (uint32_t)nd | ((uint32_t)(wave + 1) << 8);
+  store_ray_v(wb.q, i, hp, sdir, nthr, cur.item, r.n, (uint32_t)nd | ((uint32_t)(wave + 1) << 8));
   return true;
 }
 
-// One scatter site and one random_unit_vector site per shading kernel
-// (scatter_begin / scatter_end, pt_device.hpp): wf_medium's deferred
-// Perlin-textured surfaces, boundary fallbacks and medium scatters share them,
-// so each divergent piece (material scatter, rejection loop) runs once per
-// wave. A/B on MI355X against separate sites, parity-identical: C3 +0.8 %,
-// mesh fog +0.6 % (profiles/r02/ab/ab_one_scatter.log).
-
-// Per-lane tail of both shading kernels: keep a continuing ray in its slot,
-// or mark the slot of an ended path as waiting for work (the next
-// wf_intersect hands it the next item of its group's chunk).
-__device__ __forceinline__ void finish_lane(const WfBufs& wb, int32_t i, bool ended, bool go, const Ray& cont) {
-  if (go) store_ray(wb.q, i, cont);
-  if (ended) s_store(reinterpret_cast<uint32_t*>(wb.q.c + i) + 1, kPending);
+// Per-lane tail of the shading kernels for a path that ended: stage its
+// colour (0 unless it ended on an emissive boundary fallback; emissive
+// surface hits end in wf_intersect) and mark the slot as waiting for work (the
+// next wf_intersect hands it the next item).
+__device__ __forceinline__ void finish_ended(const DevFrame& fr, const WfBufs& wb, int32_t i, const Ray& ray,
+                                             pt_v3 emit) {
+  end_path(fr, wb, i, ray.item,
+           (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit) : pt_v3f(0.0f, 0.0f, 0.0f));
 }
 
-// Surface branch of shade_and_scatter (kernels.py:1359-1399) for slot ray
-// `ray` whose closest hit (t, ref) has material g.
-__device__ __forceinline__ void shade_surface(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
-                                              const Ray& ray, float t, int32_t ref, int32_t g, bool& ended,
-                                              bool& go, Ray& cont, uint32_t (&ends)[2]) {
-  Item it = decode_item(fr, wb, ray.item);
-  Rng r{path_key(fr, wb, it), ray.ctr};
-  const Mat m = load_mat(sc, g);
-  pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, t));
-  pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
-  pt_v3 emit = emitted(m);
-  pt_v3 sdir, att;
-  bool sc_ok;  // one unit-vector site for metal and isotropic lanes
-  const int32_t ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, sc_ok);
-  if (ruv != kRuvNone) sc_ok = scatter_end(sc, ruv, ref, m, hp, nrm, random_unit_vector(r), sdir, att);
-  go = scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, cont, ends);
-  if (!go) {
-    ended = true;  // an emissive hit is the path's only contribution (:1368-1375)
-    stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
-                                                                          : pt_v3f(0.0f, 0.0f, 0.0f));
+// Shard s and offset of entry j of a list whose shard segments hold cnt[s]
+// entries (cnt wave-uniform).
+__device__ __forceinline__ int32_t list_entry(const WfBufs& wb, int32_t list, const int32_t (&cnt)[kShards], int32_t j) {
+  int32_t off = j, shard = 0;
+#pragma unroll
+  for (int s = 0; s + 1 < kShards; ++s) {
+    if (shard == s && off >= cnt[s]) {
+      off -= cnt[s];
+      shard = s + 1;
+    }
   }
+  return s_load(list_slot(wb, list, shard, off));
 }
 
-// Surface hits whose scatter evaluates Perlin turbulence (a noise texture on
-// a Lambertian or isotropic material, kernels.py:1013-1015): deferred to a
-// compacted list shaded by wf_medium, so one such lane no longer puts three
-// octaves of table round trips into every wave of wf_shade that holds it.
-__device__ __forceinline__ bool noise_shaded(uint32_t flags) {
-  const uint32_t mt = flags & 0xfu, tx = (flags >> 4) & 0xfu;
-  return tx == 3u && (mt == 0u || mt == 4u);
+__device__ __forceinline__ int32_t list_counts(const WfBufs& wb, int32_t par, int32_t list, int32_t (&cnt)[kShards]) {
+  int32_t n = 0;
+#pragma unroll
+  for (int s = 0; s < kShards; ++s) {
+    cnt[s] = __builtin_amdgcn_readfirstlane(*ctl_list(wb, par, list, s));
+    n += cnt[s];
+  }
+  return n;
 }
 
-// A/B, not kept: wf_shade writing its block's continuing rays back sorted by
-// direction octant (a ray record is self-contained, so its slot is free to
-// change): -8 % C3 and mesh fog. A wave's rays come from one pixel square, and
-// that origin coherence is worth more than the direction coherence the sort
-// buys (profiles/r02/ab/ab_wf_octant_sort.log).
-
-// shade_miss_rays + shade_and_scatter for non-medium hits (kernels.py:1266-1399);
-// medium-boundary hits go to their shard's medium queue segment.
+// shade_and_scatter (kernels.py:1289-1399) for the surface hits, one
+// material per wave: the work index runs over the Lambertian, glossy and
+// dielectric lists in turn, each padded to a multiple of 64 entries, so every
+// wave shades one list — Lambertian (scatter kernels.py:829-849 + its
+// texture, :924-1017), dielectric (:876-903) or glossy (metal :853-871,
+// isotropic :905-915, and anything else scatter() receives) — and runs that
+// material's code only. The surface hit point and normal are the reference's
+// (kernels.py:1359-1364); every draw keeps the reference's order.
 #ifndef PTMI_WF_SHADE_MIN_WAVES
 #define PTMI_WF_SHADE_MIN_WAVES 5  // 96 VGPRs, no spills: A/B C3 +0.8 %; 6 waves (48 B spills) -2.7 % (profiles/r02/ab/ab_wf_occupancy.log)
 #endif
 __global__ __launch_bounds__(kWfBlock, PTMI_WF_SHADE_MIN_WAVES) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
-                                                   unsigned long long* __restrict__ counters) {
-  const Queue q = wb.q;
-  const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
-  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
-  const int32_t shard = (int32_t)(blockIdx.x % kShards);
+                                                    int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ unsigned int tally[3];
+  int32_t cnt[3][kShards], span[3];
+#pragma unroll
+  for (int l = 0; l < 3; ++l) span[l] = (list_counts(wb, par, l, cnt[l]) + 63) & ~63;
+  const int32_t n = span[0] + span[1] + span[2];
+  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < wb.capacity; base += stride) {
-    const int32_t i = base + (int32_t)threadIdx.x;
-    bool to_medium = false, to_noise = false, ended = false, go = false;
-    Ray cont;
-    const bool live = i < wb.capacity && slot_item(q, i) < kPending;
-    if (live) {
-      const float2 h = h_load(wb.hit + i);
-      const int32_t ref = __float_as_int(h.y);
-      const Ray ray = load_ray(q, i);
-      if (ref == kMissRef) {
-        stage(fr, wb, ray.item, pt_mul(ray.thr, bg));  // shade_miss_rays :1280
-        ended = true;
-      } else {
-        const int32_t g = mat_index(sc, ref);
-        const uint32_t fl = mat_flags(sc, g);
-        if ((fl >> 8) & 1u) {
-          to_medium = true;
-        } else if (noise_shaded(fl)) {
-          to_noise = true;
-        } else {
-          shade_surface(sc, fr, wb, ray, h.x, ref, g, ended, go, cont, ends);
-        }
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
+    // wave-uniform list and offset of this wave's 64 entries
+    int32_t j = base + (int32_t)threadIdx.x, list = 0;
+    if (j >= span[0]) {
+      j -= span[0];
+      list = 1;
+      if (j >= span[1]) {
+        j -= span[1];
+        list = 2;
       }
     }
-    const int32_t mslot = wave_ticket(to_medium, ctl_medium(wb, shard));
-    if (to_medium) s_store(wb.medq + shard * wb.medseg + mslot, i);
-    // deferred hits fill the shard's segment from the top; a slot is in at
-    // most one of the two lists, so together they never exceed the segment
-    const int32_t nslot = wave_ticket(to_noise, ctl_noise(wb, shard));
-    if (to_noise) s_store(wb.medq + shard * wb.medseg + wb.medseg - 1 - nslot, i);
-    finish_lane(wb, i, ended, go, cont);
-    n_ended += ended ? 1u : 0u;
+    const int32_t nl = list == 0 ? cnt[0][0] + cnt[0][1] + cnt[0][2] + cnt[0][3] + cnt[0][4] + cnt[0][5] + cnt[0][6] + cnt[0][7]
+                     : list == 1 ? cnt[1][0] + cnt[1][1] + cnt[1][2] + cnt[1][3] + cnt[1][4] + cnt[1][5] + cnt[1][6] + cnt[1][7]
+                                 : cnt[2][0] + cnt[2][1] + cnt[2][2] + cnt[2][3] + cnt[2][4] + cnt[2][5] + cnt[2][6] + cnt[2][7];
+    if (j >= nl) continue;  // the list's padding
+    const int32_t i = list == 0 ? list_entry(wb, kListLambertian, cnt[0], j)
+                    : list == 1 ? list_entry(wb, kListGlossy, cnt[1], j) : list_entry(wb, kListDielectric, cnt[2], j);
+    const float2 h = h_load(wb.hit + i);
+    const int32_t ref = __float_as_int(h.y);
+    const Ray ray = load_ray(wb.q, i);
+    const Mat m = load_mat(sc, mat_index(sc, ref));
+    Item it = decode_item(fr, wb, ray.item);
+    Rng r{path_key(fr, wb, it), ray.ctr};
+    const pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
+    const pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
+    pt_v3 sdir = pt_v3f(0.0f, 0.0f, 0.0f), att = pt_v3f(1.0f, 1.0f, 1.0f);
+    bool sc_ok = true;
+    if (list == kListLambertian) {  // kernels.py:829-849
+      att = eval_texture(sc, ref, m, hp);
+      sdir = random_cosine_direction(nrm, r);
+    } else if (list == kListDielectric) {  // kernels.py:876-903
+      sdir = scatter_dielectric(m, ray.d, nrm, r);
+    } else {
+      sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
+    }
+    const bool go = scatter_epilogue(fr, wb, i, sc_ok, hp, sdir, att, ray, r, ends);
+    if (!go) {
+      finish_ended(fr, wb, i, ray, emitted(m));
+      ++n_ended;
+    }
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, tally, counters + 2);
 }
 
 // Constant-medium rays: exit traversal + free flight (apply_constant_medium,
 // kernels.py:365-450) and the volume branch of shade_and_scatter
-// (kernels.py:1326-1357). Work index j runs over the concatenated shard segments.
+// (kernels.py:1326-1357); then the Perlin-textured surfaces. Work index j runs
+// over the medium list's shard segments, then the Perlin list's.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 #ifndef PTMI_WF_MEDIUM_MIN_WAVES
-#define PTMI_WF_MEDIUM_MIN_WAVES 4  // <= 128 VGPRs: with the deferred shading list it needs 131 otherwise (3 waves/SIMD)
+#define PTMI_WF_MEDIUM_MIN_WAVES 4  // <= 128 VGPRs: with the Perlin list it needs 131 otherwise (3 waves/SIMD)
 #endif
 __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
-                                                    unsigned long long* __restrict__ counters) {
+                                                    int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
-  int32_t cnt[kShards];  // per-shard medium counts (wave-uniform)
-  int32_t n = 0;
-#pragma unroll
-  for (int s = 0; s < kShards; ++s) {
-    cnt[s] = __builtin_amdgcn_readfirstlane(*ctl_medium(wb, s));
-    n += cnt[s];
-  }
+  int32_t cnt[kShards], cntn[kShards];  // per-shard medium / Perlin counts (wave-uniform)
+  const int32_t n = list_counts(wb, par, kListMedium, cnt);
+  const int32_t nn = list_counts(wb, par, kListNoise, cntn);
+  if (blockIdx.x < kShards && threadIdx.x < kLists)  // the next iteration's lists start empty
+    *ctl_list(wb, par ^ 1, (int32_t)threadIdx.x, (int32_t)blockIdx.x) = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
-  int32_t nn = 0;  // deferred surface hits (wf_shade), after the medium rays in the index space
-  int32_t cntn[kShards];
-#pragma unroll
-  for (int s = 0; s < kShards; ++s) {
-    cntn[s] = __builtin_amdgcn_readfirstlane(*ctl_noise(wb, s));
-    nn += cntn[s];
-  }
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0, ends[2] = {0u, 0u};
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
     const int32_t j = base + (int32_t)threadIdx.x;
     bool ended = false, go = false;
-    Ray cont;
-    int32_t i = -1, shard = 0;
+    pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
+    int32_t i = -1;
     const bool is_noise = j >= n && j < n + nn;
-    if (j < n) {  // medium-queue slot
-      int32_t off = j;
-#pragma unroll
-      for (int s = 0; s + 1 < kShards; ++s) {
-        if (shard == s && off >= cnt[s]) {
-          off -= cnt[s];
-          shard = s + 1;
-        }
-      }
-      i = s_load(wb.medq + shard * wb.medseg + off);
-    } else if (is_noise) {  // deferred surface slot (wf_shade), from the top of the segment
-      int32_t off = j - n;
-#pragma unroll
-      for (int s = 0; s + 1 < kShards; ++s) {
-        if (shard == s && off >= cntn[s]) {
-          off -= cntn[s];
-          shard = s + 1;
-        }
-      }
-      i = s_load(wb.medq + shard * wb.medseg + wb.medseg - 1 - off);
-    }
+    if (j < n) i = list_entry(wb, kListMedium, cnt, j);
+    else if (is_noise) i = list_entry(wb, kListNoise, cntn, j - n);
     if (i >= 0) {
       const float2 h = h_load(wb.hit + i);
       const int32_t ref = __float_as_int(h.y);
@@ -590,7 +664,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
       Rng r{path_key(fr, wb, it), ray.ctr};
       bool surface = is_noise, scattered = false, passthrough = false;
       int32_t ruv = kRuvNone;
-      pt_v3 hp, nrm, sdir, att, emit = pt_v3f(0.0f, 0.0f, 0.0f);
+      pt_v3 hp, nrm, sdir, att;
       if (!is_noise) {
         float t_exit;
         pt_v3 mp;
@@ -606,17 +680,15 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
             ++ends[1];  // Q14: no wave left for the passthrough
           } else {
             float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
-            cont = ray;
-            cont.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
-            cont.ctr = r.n;
-            cont.meta = ray.meta + (1u << 8);
+            store_ray_v(wb.q, i, pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t)), ray.d, ray.thr, ray.item, r.n,
+                        ray.meta + (1u << 8));
             go = true;
           }
         } else {  // fallback: the boundary as a surface (kernels.py:1352-1357)
           surface = true;
         }
       }
-      if (surface) {  // one scatter site: deferred Perlin-textured hits and boundary fallbacks
+      if (surface) {  // one scatter site: Perlin-textured hits and boundary fallbacks
         hp = pt_add(ray.o, pt_scale(ray.d, h.x));
         nrm = hit_normal(sc, ref, hp, ray.d);
         emit = emitted(m);
@@ -627,14 +699,10 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(
         if (ruv == kRuvMedium) sdir = v;
         else scattered = scatter_end(sc, ruv, ref, m, hp, nrm, v, sdir, att);
       }
-      if (!passthrough) go = scatter_epilogue(fr, scattered, hp, sdir, att, ray, r, cont, ends);
-      if (!go) {
-        ended = true;  // emissive surfaces add their emission once (:1368-1375); other ends add 0
-        stage(fr, wb, ray.item, (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit)
-                                                                              : pt_v3f(0.0f, 0.0f, 0.0f));
-      }
+      if (!passthrough) go = scatter_epilogue(fr, wb, i, scattered, hp, sdir, att, ray, r, ends);
+      ended = !go;
+      if (ended) finish_ended(fr, wb, i, ray, emit);
     }
-    finish_lane(wb, i, ended, go, cont);
     n_ended += ended ? 1u : 0u;
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
@@ -685,7 +753,7 @@ constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
 struct Layout {
   int32_t capacity, medseg;
-  size_t q, hit, medq, grp, staging, ctl, total;
+  size_t q, hit, lists, grp, staging, ctl, total;
 };
 
 Layout layout(int32_t npix, int32_t batch) {
@@ -699,8 +767,8 @@ Layout layout(int32_t npix, int32_t batch) {
   size_t c = (size_t)cap;
   L.q = 0;
   L.hit = L.q + 3 * sizeof(float4) * c;
-  L.medq = L.hit + sizeof(float2) * c;
-  L.grp = (L.medq + sizeof(int32_t) * c + 15) & ~(size_t)15;
+  L.lists = L.hit + sizeof(float2) * c;
+  L.grp = (L.lists + 4 * sizeof(int32_t) * c + 15) & ~(size_t)15;
   L.staging = (L.grp + sizeof(int2) * (c / 64) + 15) & ~(size_t)15;
   L.ctl = (L.staging + 3 * sizeof(float) * (size_t)items + 255) & ~(size_t)255;
   L.total = L.ctl + kCtlWords * sizeof(int32_t);
@@ -759,14 +827,15 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
       for (int p = 0; p < kPipes; ++p) {
         if (!live[p]) continue;
         const WfBufs& wb = wbs[p];
+        const int32_t par = (int32_t)((it + j) & 1);  // which list counters this iteration uses
         prof_begin(kProfWfIntersect, st[p]);
-        hipLaunchKernelGGL((wf_intersect<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        hipLaunchKernelGGL((wf_intersect<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
         prof_end(kProfWfIntersect, st[p]);
         prof_begin(kProfWfShade, st[p]);
-        hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
         prof_end(kProfWfShade, st[p]);
         prof_begin(kProfWfMedium, st[p]);
-        hipLaunchKernelGGL((wf_medium<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, counters);
+        hipLaunchKernelGGL((wf_medium<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
         prof_end(kProfWfMedium, st[p]);
       }
     }
@@ -853,7 +922,7 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
       wb.q.b = (float4*)(base + L.q + sizeof(float4) * c) + p * cp;
       wb.q.c = (float4*)(base + L.q + 2 * sizeof(float4) * c) + p * cp;
       wb.hit = (float2*)(base + L.hit) + p * cp;
-      wb.medq = (int32_t*)(base + L.medq) + p * cp;
+      wb.lists = (int32_t*)(base + L.lists) + p * 4 * cp;
       wb.grp = (int2*)(base + L.grp) + p * (cp / 64);
       wb.staging = (float*)(base + L.staging);
       wb.next = (int32_t*)(base + L.ctl);
@@ -869,6 +938,9 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
       wb.shard_len = (wb.nunits / wb.csamp + kShards - 1) / kShards * wb.csamp;
       wb.shard_groups = L.capacity / 64 / kShards;  // all pipes draw on every shard
       wb.s_begin = s_begin + b0;
+      wb.by_per = fast_div(64u * (uint32_t)wb.csamp);
+      wb.by_nsq = fast_div((uint32_t)wb.nsq);
+      wb.by_sqx = fast_div((uint32_t)wb.sq_x);
     }
     hipError_t e;
     if (fr.traversal == PTMI_TRAV_STACKLESS) e = wf_batch<1, PTMI_TRAV_STACKLESS>(sc, fr, wbs, accum, nb, counters, stream, *ps);

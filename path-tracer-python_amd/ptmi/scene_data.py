@@ -171,16 +171,38 @@ def fixture_manifest():
 
 # ---------------------------------------------------------------- packing
 LEAF_FLAG = np.int64(0x80000000)
+LEAF_INDEX_BITS = 25  # leaf code: flag | type << 28 | material class << 25 | primitive index
+MAX_PRIMS_PER_TYPE = 1 << LEAF_INDEX_BITS
+
+# Material class of a leaf (include/ptmi.h PTMI_CLASS_*): which of the
+# wavefront's shading lists a hit on it goes to, decided once per primitive
+# from its material flags instead of by a dependent load after every traversal.
+CLASS_LAMBERTIAN, CLASS_GLOSSY, CLASS_DIELECTRIC, CLASS_MEDIUM, CLASS_NOISE, CLASS_EMISSIVE = range(6)
 
 
 NODE_FLOATS = 20  # 80-B internal node (include/ptmi.h)
 NODE_BYTES = 4 * NODE_FLOATS  # an internal child ref is the child's byte offset in the node array
-PACKET_BYTES = 256  # two-level node packet: 3 child records + 16 B padding
 
 
-def leaf_code(prim_type, prim_idx):
-    code = LEAF_FLAG | (np.int64(prim_type) << 28) | np.int64(prim_idx)
+def leaf_code(prim_type, prim_idx, mat_class=0):
+    code = LEAF_FLAG | (np.int64(prim_type) << 28) | (np.int64(mat_class) << LEAF_INDEX_BITS) | np.int64(prim_idx)
     return np.int32(np.int64(code) - (1 << 32))  # as signed int32 bits
+
+
+def material_class(flags):
+    """Class of packed material flags (mt | tex << 4 | medium << 8 | ...):
+    medium boundary; Perlin-textured Lambertian or isotropic (noise); then by
+    material type: Lambertian 0, dielectric 2, emissive 3, else glossy (metal
+    1, isotropic 4, unknown: scatter() decides)."""
+    flags = np.asarray(flags, np.uint32).astype(np.int64)
+    mt, tt, med = flags & 0xf, (flags >> 4) & 0xf, (flags >> 8) & 1
+    cls = np.full(flags.shape, CLASS_GLOSSY, np.int64)
+    cls[mt == 0] = CLASS_LAMBERTIAN
+    cls[mt == 2] = CLASS_DIELECTRIC
+    cls[mt == 3] = CLASS_EMISSIVE
+    cls[(tt == 3) & ((mt == 0) | (mt == 4))] = CLASS_NOISE
+    cls[med == 1] = CLASS_MEDIUM
+    return cls
 
 
 @dataclass
@@ -321,10 +343,9 @@ def ref_layout_nodes(bvh, codes):
 
 def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True) -> DeviceLayout:
     """Reference-layout arrays -> include/ptmi.h device layout. ``node_bytes``
-    is the library's node stride (ptmi_node_bytes()): 80 for one child record
-    per internal node, 256 for two-level packets (record 0: the node's
-    children; records 1 and 2: each child's children, zero for a leaf
-    child). ``leaf_order`` renumbers each primitive type in BVH leaf order
+    is the library's node stride (ptmi_node_bytes(): 80, one child record
+    per internal node). Each leaf code carries its primitive's material
+    class (material_class). ``leaf_order`` renumbers each primitive type in BVH leaf order
     (leaf_order_perm); leaf codes, primitive and material rows are permuted
     together, so every lookup the kernels make finds the same data and the
     traversal visits the same leaves in the same order: results are
@@ -354,8 +375,19 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
         inv[perm[t]] = np.arange(counts[t])
         sel = is_leaf & (ptype == t)
         new_idx[sel] = inv[pidx[sel]]
-    codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | new_idx) - (1 << 32)).astype(np.int32)
-    if node_bytes not in (NODE_BYTES, PACKET_BYTES):
+    if max(counts) > MAX_PRIMS_PER_TYPE:
+        raise ValueError(f'at most {MAX_PRIMS_PER_TYPE} primitives of one type (25-bit leaf index)')
+    ps, pt, pq = perm
+    mats = np.concatenate([_pack_mats(sa.sphere_mats, ns)[ps], _pack_mats(sa.quad_mats, nq)[pq],
+                           _pack_mats(sa.tri_mats, nt)[pt]], axis=0)
+    mat_base = np.array([0, ns + nq, ns], np.int64)  # mats rows: spheres | quads | triangles, by type code
+    cls = np.zeros(n, np.int64)
+    if n:
+        rows = mat_base[np.where(is_leaf, ptype, 0)] + np.where(is_leaf, new_idx, 0)
+        cls = np.where(is_leaf, material_class(mats[rows, 19].view(np.uint32)) if len(mats) else 0, 0)
+    codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | (cls << LEAF_INDEX_BITS) | new_idx)
+             - (1 << 32)).astype(np.int32)
+    if node_bytes != NODE_BYTES:
         raise ValueError(f'unsupported node stride {node_bytes}')
     if internal.shape[0] * node_bytes > 0x7fffffff:
         raise ValueError(f'{internal.shape[0]} internal BVH nodes: byte offsets exceed int32')
@@ -374,14 +406,6 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
         nodes[:, 14], nodes[:, 15] = cl[:, 2], cr[:, 2]
         nodes[:, 16], nodes[:, 17] = cl[:, 0], cr[:, 0]
         nodes[:, 18], nodes[:, 19] = cl[:, 1], cr[:, 1]
-    if node_bytes == PACKET_BYTES:  # two-level packets: the node's record, then each internal child's
-        pk = np.zeros((internal.shape[0], PACKET_BYTES // 4), np.float32)
-        pk[:, :NODE_FLOATS] = nodes
-        if internal.size:
-            for k, ch in ((1, left[internal]), (2, right[internal])):
-                inner = cidx[ch] >= 0
-                pk[inner, k * NODE_FLOATS:(k + 1) * NODE_FLOATS] = nodes[cidx[ch[inner]]]
-        nodes = pk
     ref_nodes = ref_layout_nodes(b, np.where(is_leaf, codes, 0).astype(np.int32))
     if n:
         root_ref = int(refs[0])
@@ -389,7 +413,6 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
         max_leaf_depth = int(leaf_depths(b).max())
     else:
         root_ref, root_min, root_max, max_leaf_depth = 0, np.zeros(3, np.float32), np.zeros(3, np.float32), 0
-    ps, pt, pq = perm
     spheres = np.ascontiguousarray(np.asarray(sa.sphere_data, np.float32).reshape(ns, 4)[ps])
     q = sa.quads
     quads = np.zeros((nq, 16), np.float32)
@@ -406,8 +429,6 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
     tris[:, 6:9] = t['triangle_edge2']
     tris[:, 9:12] = t['triangle_normal']
     quads, tris = quads[pq], tris[pt]
-    mats = np.concatenate([_pack_mats(sa.sphere_mats, ns)[ps], _pack_mats(sa.quad_mats, nq)[pq],
-                           _pack_mats(sa.tri_mats, nt)[pt]], axis=0)
     if len(sa.images) > MAX_IMAGES:
         raise ValueError(f'at most {MAX_IMAGES} image textures')
     texels, offs, ws, hs, off = [], [], [], [], 0
