@@ -336,7 +336,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           done = true;
         } else {
           g = mat_index(sc, ref);
-          if ((mat_flags(sc, g) >> 8) & 1u) {  // medium boundary: exit search next segment
+          if (leaf_class(ref) == PTMI_CLASS_MEDIUM) {  // medium boundary (class in the leaf code): exit search next
             ps.mode = kModeMediumExit;
             ps.t_entry = t;
             ps.ref_entry = ref;
