@@ -131,6 +131,12 @@ constexpr int kMkBlock = 64;
 #ifndef PTMI_MK_CHUNK_SAMPLES
 #define PTMI_MK_CHUNK_SAMPLES 32  // A/B (C2, C4): 32/4 ~ 16/4 ~ 64/4 > 16/2, 16/8, 8/4 >> 64/2
 #endif
+#ifndef PTMI_MK_TAIL_DIV_SMALL
+#define PTMI_MK_TAIL_DIV_SMALL 2  // ... for batches of fewer than PTMI_MK_SMALL_BATCH samples
+#endif
+#ifndef PTMI_MK_SMALL_BATCH
+#define PTMI_MK_SMALL_BATCH 8000000
+#endif
 #ifndef PTMI_MK_TAIL_DIV
 #define PTMI_MK_TAIL_DIV 4  // a fetch takes at most (units left) / (TAIL_DIV * waves) units
                             // (re-tuned: 2 is +3 % on C2 but -8 % on C4's long fog paths;
@@ -635,7 +641,12 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   int64_t waves = (int64_t)(per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
   const int64_t chunks = wk.nunits;
   if (waves > chunks) waves = chunks;
-  const int64_t tdiv = PTMI_MK_TAIL_DIV * waves / kMkShards;  // per shard: the waves pulling from it
+  // per shard: the waves pulling from it. Small batches (a multi-GPU tile
+  // shard: 5 M samples per call for vol2 at 8 GPUs) are all tail: halving the
+  // divisor there takes larger fetches, so a wave changes tile less often
+  // (A/B, 8-rank rehearsal: +2 % per GPU; profiles/r03/ab/ab_mk_small_calls.log).
+  const int64_t tail = (int64_t)fr.w * fr.n_rows * nb < PTMI_MK_SMALL_BATCH ? PTMI_MK_TAIL_DIV_SMALL : PTMI_MK_TAIL_DIV;
+  const int64_t tdiv = tail * waves / kMkShards;
   wk.tail_div = (int32_t)(tdiv > 1 ? tdiv : 1);
   (void)hipMemsetAsync(wk.ctl, 0, 256 * kMkShards, stream);
   prof_begin(kProfMk, stream);
