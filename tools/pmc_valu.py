@@ -10,7 +10,12 @@ Per the largest mk_render_kernel dispatch of the run:
   lane_efficiency = SQ_THREAD_CYCLES_VALU / (64 * SQ_INSTS_VALU)
   wait_frac       = SQ_WAIT_ANY / SQ_WAVE_CYCLES,  issue_frac = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
 Writes profiles/valu.json[KEY] (KEY = scene:width:variant:kernel, as bench.py looks it up).
-usage: pmc_valu.py [KEY] [DIR]"""
+usage: pmc_valu.py [KEY] [DIR] [PREFIX] [KERNEL_SUBSTR]
+PREFIX: the passes' file prefix (mk, wf); KERNEL_SUBSTR: the kernel (default
+mk_render_kernel). A kernel launched many times (the wavefront's stages) is
+summed over all its dispatches instead of taking the largest one (rocprofv3
+serialises dispatches while it collects counters, so the sums are that
+kernel's own)."""
 import collections
 import csv
 import json
@@ -23,17 +28,25 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
 def main():
     key = sys.argv[1] if len(sys.argv) > 1 else 'vol2_final_scene:800:mk:megakernel'
     d = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, 'profiles', 'r01', 'pmc_latency')
+    prefix = sys.argv[3] if len(sys.argv) > 3 else 'mk'
+    kern = sys.argv[4] if len(sys.argv) > 4 else 'mk_render_kernel'
     per = collections.defaultdict(dict)
     for p in 'abc':
-        with open(os.path.join(d, f'mk_{p}_counter_collection.csv')) as f:
+        with open(os.path.join(d, f'{prefix}_{p}_counter_collection.csv')) as f:
             for r in csv.DictReader(f):
-                if 'mk_render_kernel' in r['Kernel_Name']:
+                if kern in r['Kernel_Name']:
                     c = per[(p, r['Dispatch_Id'])]
                     c[r['Counter_Name']] = c.get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
     v = {}
-    for p in 'abc':  # the largest dispatch of each pass (same launch in every pass)
+    for p in 'abc':
         runs = [c for (q, _), c in per.items() if q == p]
-        v.update(max(runs, key=lambda c: max(c.values())))
+        if kern == 'mk_render_kernel':  # the largest dispatch of each pass (same launch in every pass)
+            v.update(max(runs, key=lambda c: max(c.values())))
+        else:  # every dispatch of the kernel
+            tot = collections.Counter()
+            for c in runs:
+                tot.update(c)
+            v.update(tot)
     cycles = v['GRBM_GUI_ACTIVE'] / 8
     out = {
         'valu_issue_frac': round(2 * v['SQ_INSTS_VALU'] / (1024 * cycles), 4),
@@ -42,8 +55,8 @@ def main():
         'wave_issue_frac': round(v['SQ_ACTIVE_INST_ANY'] / v['SQ_WAVE_CYCLES'], 4),
         'valu_insts': v['SQ_INSTS_VALU'],
         'kernel_ms': round(cycles / 2.4e6, 3),
-        'source': os.path.relpath(d, ROOT) + '/mk_{a,b,c}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
-                  'tools/ab.py mk 32 1, one 32-spp launch); tools/pmc_valu.py',
+        'source': os.path.relpath(d, ROOT) + f'/{prefix}_{{a,b,c}}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
+                  f'tools/ab.py {prefix} 32 1, one 32-spp call; kernel {kern}); tools/pmc_valu.py',
     }
     path = os.path.join(ROOT, 'profiles', 'valu.json')
     rows = {}
