@@ -247,8 +247,9 @@ int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int
  * then record around every kernel; ptmi_prof_stop synchronises, returns the
  * summed milliseconds and launch counts per kernel kind
  * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 wf_shade, 4 wf_medium,
- * 5 wf_resolve, 6 mk_resolve} and disables timing. Not thread-safe; one
- * profiling session per process. */
+ * 5 wf_resolve, 6 mk_resolve} and disables timing. One profiling session
+ * per process; render calls from several host threads may record into it
+ * (each launch owns its event pair; the session is mutex-guarded). */
 #define PTMI_PROF_KINDS 7
 int ptmi_prof_start(int32_t max_launches);
 int ptmi_prof_stop(double *ms_by_kernel, uint64_t *launches_by_kernel, int32_t n_kinds);

@@ -563,9 +563,9 @@ hipError_t launch_stage_resolve(const DevFrame& fr, const float* staging, int32_
                                 float* accum, int prof_kind, hipStream_t stream) {
   unsigned g = (unsigned)((npix + kBlock - 1) / kBlock);
   if (g > 2048) g = 2048;
-  prof_begin(prof_kind, stream);
+  const int pslot = prof_begin(prof_kind, stream);
   hipLaunchKernelGGL(stage_resolve, dim3(g), dim3(kBlock), 0, stream, fr, staging, npix, batch, accum);
-  prof_end(prof_kind, stream);
+  prof_end(pslot, stream);
   return hipGetLastError();
 }
 
@@ -573,10 +573,10 @@ template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t launch_mk(const DevScene& sc, const DevFrame& fr, float* accum, int32_t s_begin,
                             int32_t s_count, unsigned long long* counters, hipStream_t stream) {
   dim3 grid((unsigned)((fr.w + kMkTile - 1) / kMkTile), (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile));
-  prof_begin(kProfMk, stream);
+  const int pslot = prof_begin(kProfMk, stream);
   hipLaunchKernelGGL((mk_render_kernel<STACK, false, TRAV>), grid, dim3(kMkBlock), 0, stream, sc, fr, accum, s_begin,
                      s_count, s_count, (float*)nullptr, counters, MkWork{});
-  prof_end(kProfMk, stream);
+  prof_end(pslot, stream);
   return hipGetLastError();
 }
 
@@ -649,10 +649,10 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   const int64_t tdiv = tail * waves / kMkShards;
   wk.tail_div = (int32_t)(tdiv > 1 ? tdiv : 1);
   (void)hipMemsetAsync(wk.ctl, 0, 256 * kMkShards, stream);
-  prof_begin(kProfMk, stream);
+  const int pslot = prof_begin(kProfMk, stream);
   hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, nb, staging, counters, wk);
-  prof_end(kProfMk, stream);
+  prof_end(pslot, stream);
   return hipGetLastError();
 }
 

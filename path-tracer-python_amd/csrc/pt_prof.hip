@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -21,26 +22,32 @@ struct Prof {
   bool overflow = false;
 };
 Prof g_prof;
+std::mutex g_prof_mu;  // one session per process, used from any host thread
 }  // namespace
 
-void prof_begin(int32_t kind, hipStream_t s) {
-  if (!g_prof.on) return;
+int prof_begin(int32_t kind, hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_prof_mu);
+  if (!g_prof.on) return -1;
   if (g_prof.used + 2 > g_prof.ev.size()) {
     g_prof.overflow = true;
-    return;
+    return -1;
   }
+  const int slot = (int)(g_prof.used / 2);
   g_prof.kind.push_back(kind);
-  (void)hipEventRecord(g_prof.ev[g_prof.used], s);
+  g_prof.used += 2;
+  (void)hipEventRecord(g_prof.ev[2 * (size_t)slot], s);
+  return slot;
 }
 
-void prof_end(int32_t kind, hipStream_t s) {
-  (void)kind;
-  if (!g_prof.on || g_prof.used + 2 > g_prof.ev.size()) return;
-  (void)hipEventRecord(g_prof.ev[g_prof.used + 1], s);
-  g_prof.used += 2;
+void prof_end(int slot, hipStream_t s) {
+  if (slot < 0) return;
+  std::lock_guard<std::mutex> lock(g_prof_mu);
+  if (!g_prof.on || 2 * (size_t)slot + 1 >= g_prof.ev.size()) return;
+  (void)hipEventRecord(g_prof.ev[2 * (size_t)slot + 1], s);
 }
 
 int prof_start(int32_t max_launches) {
+  std::lock_guard<std::mutex> lock(g_prof_mu);
   for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
   g_prof = Prof();
   if (max_launches <= 0) return 0;
@@ -58,6 +65,7 @@ int prof_start(int32_t max_launches) {
 // on two streams, the wavefront's pipes) count once there, so busy / launches
 // is the GPU time per launch, while ms sums each launch's own duration.
 int prof_stop(double* ms, double* busy, uint64_t* launches, int32_t n_kinds) {
+  std::lock_guard<std::mutex> lock(g_prof_mu);
   for (int32_t k = 0; k < n_kinds; ++k) {
     ms[k] = 0.0;
     launches[k] = 0;

@@ -794,9 +794,9 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
   const unsigned g = (unsigned)blocks;
   (void)hipMemsetAsync(wbs[0].next, 0, kCtlWords * sizeof(int32_t), stream);
   for (int p = 0; p < kPipes; ++p) {
-    prof_begin(kProfWfGenerate, stream);
+    const int pslot = prof_begin(kProfWfGenerate, stream);
     hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kWfBlock), 0, stream, fr, wbs[p], (int32_t)(p == 0));
-    prof_end(kProfWfGenerate, stream);
+    prof_end(pslot, stream);
   }
   hipStream_t st[kPipes];
   st[0] = stream;
@@ -828,15 +828,15 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
         if (!live[p]) continue;
         const WfBufs& wb = wbs[p];
         const int32_t par = (int32_t)((it + j) & 1);  // which list counters this iteration uses
-        prof_begin(kProfWfIntersect, st[p]);
+        const int ps_i = prof_begin(kProfWfIntersect, st[p]);
         hipLaunchKernelGGL((wf_intersect<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
-        prof_end(kProfWfIntersect, st[p]);
-        prof_begin(kProfWfShade, st[p]);
+        prof_end(ps_i, st[p]);
+        const int ps_s = prof_begin(kProfWfShade, st[p]);
         hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
-        prof_end(kProfWfShade, st[p]);
-        prof_begin(kProfWfMedium, st[p]);
+        prof_end(ps_s, st[p]);
+        const int ps_m = prof_begin(kProfWfMedium, st[p]);
         hipLaunchKernelGGL((wf_medium<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
-        prof_end(kProfWfMedium, st[p]);
+        prof_end(ps_m, st[p]);
       }
     }
     it += n;

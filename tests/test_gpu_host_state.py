@@ -213,3 +213,46 @@ def test_mk_overlapped_calls_on_changing_streams():
     torch.cuda.synchronize()
     assert torch.equal(acc, ref)
     assert integ.read_counters() == want_cnt
+
+
+def test_profiler_with_concurrent_megakernel_threads():
+    """ptmi_prof_* with render calls from several host threads: every launch
+    gets its own event pair (no mixed-up begin/end), so the launch counts are
+    exact and every duration is positive and bounded by the session."""
+    import time
+    import torch
+    from ptmi import device, _lib
+    sa, cam, _ = scene_inputs('vol2_final_scene', 800)
+    dscene = device.DeviceScene.from_arrays(sa)
+    n, calls = 3, 4
+    integs = [device.Integrator(dscene) for _ in range(n)]
+    accs = [_frame_acc(cam, (0, 0, 800, 800)) for _ in range(n)]
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    for k in range(n):  # warm-up: workspaces
+        integs[k].render_mk(accs[k][0], accs[k][1], 0, 2, stream=streams[k])
+    torch.cuda.synchronize()
+    errors = []
+    start = threading.Barrier(n)
+
+    def work(k):
+        try:
+            start.wait()
+            for c in range(calls):
+                integs[k].render_mk(accs[k][0], accs[k][1], 2 + 4 * c, 4, stream=streams[k])
+            streams[k].synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    with _lib.KernelTimer(max_launches=1000) as kt:
+        t0 = time.perf_counter()
+        threads = [threading.Thread(target=work, args=(k,)) for k in range(n)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=120)
+        torch.cuda.synchronize()
+        wall_ms = (time.perf_counter() - t0) * 1e3
+    assert not errors, errors
+    mk, res = kt.result['megakernel'], kt.result['mk_resolve']
+    assert mk['launches'] == n * calls == res['launches'] and not kt.truncated
+    assert 0.0 < mk['busy_ms'] <= min(mk['ms'], wall_ms * 1.02 + 0.1)
