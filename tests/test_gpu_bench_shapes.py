@@ -4,7 +4,8 @@ The window tests (test_gpu_parity.py) render small frames from sample 0 with
 1-8 spp per call. bench.py's timed region runs differently: whole frames,
 64 (C2, C3), 32 (C4) or 16 (C5) samples per call at sample indices in the
 hundreds or thousands, through the persistent staged megakernel with
-overlapped launches (two traces in flight, 8 unit shards with stealing), or
+overlapped launches (two or three traces in flight, 8 unit shards with
+stealing), or
 the 4-pipe wavefront. These tests drive bench.BenchRun — the object bench.py
 times — exactly as bench.py does and compare the result against the CPU
 oracle (oracle/, test infrastructure only):
@@ -65,13 +66,15 @@ def oracle_windows(run, windows, s_begin, s_count):
 
 
 def windows_of(run, n=5, size=64, seed=7):
-    """Deterministic scattered windows: the centre plus n-1 random ones."""
+    """Deterministic scattered windows: the centre plus n-1 random ones, none
+    overlapping another (the oracle renders them all into one accumulator)."""
     W, H = run.W, run.H
     rng = np.random.default_rng(seed)
     wins = [((W - size) // 2, (H - size) // 2, size, size)]
     while len(wins) < n:
         x, y = int(rng.integers(0, W - size + 1)), int(rng.integers(0, H - size + 1))
-        wins.append((x, y, size, size))
+        if all(abs(x - u) >= size or abs(y - v) >= size for u, v, _, _ in wins):
+            wins.append((x, y, size, size))
     return wins
 
 
@@ -175,3 +178,21 @@ def test_eight_rank_tile_partition_is_bit_identical(preset):
     torch.cuda.synchronize()
     assert (rows_seen == 1).all()  # every row rendered by exactly one rank
     assert torch.equal(parts, full)
+
+
+@pytest.mark.parametrize('preset', ['c2', 'c3'])
+def test_stackless_traversal_at_the_bench_call_shape(preset):
+    """bench.py --traversal stackless (the reference's USE_STACKLESS_TRAVERSAL
+    walk, kernels.py:453-597): three consecutive calls from sample 1536 on
+    scattered windows, against the oracle's stackless restatement."""
+    import torch
+    run = bench_run(preset, ('--traversal', 'stackless'))
+    acc = torch.zeros((run.H, run.W, 3), dtype=torch.float32, device='cuda')
+    steps = steps_of(run, 3)
+    for k in steps:
+        run.step(acc, k)
+    torch.cuda.synchronize()
+    g = acc.cpu().numpy()
+    wins = windows_of(run, 4, seed=5)
+    o, _ = oracle_windows(run, wins, S0, 3 * run.sps)
+    check_windows(g, o, wins, 3 * run.sps, f'{preset} stackless calls {steps}')
