@@ -186,8 +186,12 @@ class Integrator:
                                                self._cnt(), self._stream(stream)),
                        'ptmi_mk_render')
 
-    # staging budget for the per-(sample, pixel) colour slots of one batch
-    STAGING_BYTES = 1 << 30
+    # Staging budget for the per-(sample, pixel) colour slots of one batch:
+    # 2 GiB keeps a whole 16-spp 4K call (1.6 GB) in one batch. A/B on MI355X
+    # (PTMI_STAGING_BYTES, A/B only): C5 3757 (1 GiB: 10 + 6 spp batches) ->
+    # 3788 Msamples/s, C2 unchanged, 4 GiB no further change
+    # (profiles/r03/ab/ab_staging_bytes.log).
+    STAGING_BYTES = int(os.environ.get('PTMI_STAGING_BYTES', str(2 << 30)))
     # Overlapped megakernel calls: traces in flight, one workspace and side
     # stream each. Two for full-frame calls; three for small calls, whose
     # drain is a larger part of a launch. A/B on MI355X (vol2 800x800, 64 spp
