@@ -166,13 +166,35 @@ struct MkWork {
   int32_t* ctl;      // kMkShards counters, one per 256-B line: units taken from each shard (zeroed before the launch)
   int32_t shard_len; // units per shard (the last one may be short)
   int32_t csamp;     // most units per fetch
-  int32_t tiles_x;   // 8x8 tiles per row
+  int32_t tiles_x;   // 64-pixel tiles per row
+  int32_t tw_log2;   // tile width log2: 3 for 8x8 tiles, 4 for 16x4, 5 for 32x2, 6 for 64x1
   int32_t nb;        // samples of the batch (units per tile)
   FastDiv by_nb, by_tiles_x, by_len;
   int32_t nunits;    // units of the batch (multiple of csamp)
   int32_t tail_div;  // TAIL_DIV * waves of the grid
 };
 constexpr int kMkTile = 8;
+
+#ifndef PTMI_MK_BAND_TILES
+#define PTMI_MK_BAND_TILES 1
+#endif
+// Tile height (log2) of the staged megakernel's 64-pixel tiles. A frame's
+// local rows are its row bands packed together, so an 8x8 tile over 4-row
+// bands (bench.py --gpus 8 at 800 rows) would cover two runs of 4 image rows
+// 32 rows apart; a tile as tall as the band's largest power-of-two divisor
+// (16x4, 32x2, 64x1) stays inside one band. Which lane renders which pixel
+// changes nothing in the image (staging[sample][pixel], ordered resolve).
+static int mk_tile_rows_log2(const DevFrame& fr) {
+  if (!PTMI_MK_BAND_TILES || fr.band_stride <= 1) return 3;
+  const int32_t th = fr.band_rows & -fr.band_rows;
+  return th >= 8 ? 3 : th >= 4 ? 2 : th >= 2 ? 1 : 0;
+}
+static int64_t mk_tiles(const DevFrame& fr, int32_t* tx_out = nullptr) {
+  const int hl = mk_tile_rows_log2(fr), tw = 64 >> hl, th = 1 << hl;
+  const int64_t tx = (fr.w + tw - 1) / tw, ty = (fr.n_rows + th - 1) / th;
+  if (tx_out) *tx_out = (int32_t)tx;
+  return tx * ty;
+}
 
 template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
@@ -236,7 +258,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // shard-contiguous unit numbering: shard s holds tiles s, s + S, s + 2S, ...
       const uint32_t v = k >> 6, sh = fdiv(v, wk.by_len), j = v - sh * (uint32_t)wk.shard_len;
       const uint32_t tq = fdiv(j, wk.by_nb), t = tq * (uint32_t)kMkShards + sh, ty = fdiv(t, wk.by_tiles_x);
-      return Loc{fr.x0 + (int32_t)(t - ty * (uint32_t)wk.tiles_x) * 8, (int32_t)ty * 8,
+      return Loc{fr.x0 + ((int32_t)(t - ty * (uint32_t)wk.tiles_x) << wk.tw_log2), (int32_t)ty << (6 - wk.tw_log2),
                  s_begin + (int32_t)(j - tq * (uint32_t)wk.nb)};
     }
     return Loc{sq_x, sq_y, s0 + (int32_t)(k >> 6)};
@@ -245,8 +267,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     const int32_t p = (int32_t)(k & 63u);
     const Loc l = locate(k);
     s = l.s;
-    px = l.x + (p & 7);
-    lr = l.row + (p >> 3);
+    const int twl = kPersist ? wk.tw_log2 : 3;
+    px = l.x + (p & ((1 << twl) - 1));
+    lr = l.row + (p >> twl);
     py = (lr < fr.n_rows && px < fr.x0 + fr.w && s < s_begin + s_count) ? frame_row(fr, lr) : -1;
     if (STAGED) slot = (uint32_t)(s - s_begin) * (uint32_t)npix + (uint32_t)lr * (uint32_t)fr.w + (uint32_t)(px - fr.x0);
     return py >= 0;
@@ -612,8 +635,8 @@ template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float* staging, int32_t s_begin,
                                   int32_t nb, unsigned long long* counters, hipStream_t stream) {
   float* accum = nullptr;  // staged kernels write staging only
-  const unsigned tx = (unsigned)((fr.w + kMkTile - 1) / kMkTile), ty = (unsigned)((fr.n_rows + kMkTile - 1) / kMkTile);
-  const int64_t tiles = (int64_t)tx * ty;
+  int32_t tx = 0;
+  const int64_t tiles = mk_tiles(fr, &tx);
   int dev = 0, ncu = 0, per_cu = 0;
   hipError_t e0 = hipGetDevice(&dev);
   if (e0 == hipSuccess) e0 = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -623,7 +646,8 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   MkWork wk;
   wk.ctl = (int32_t*)((char*)staging + mk_staging_bytes(fr.w * fr.n_rows, nb));
   wk.csamp = PTMI_MK_CHUNK_SAMPLES;
-  wk.tiles_x = (int32_t)tx;
+  wk.tiles_x = tx;
+  wk.tw_log2 = 6 - mk_tile_rows_log2(fr);
   wk.nb = nb;
   if (tiles * nb * 64 >= (1ll << 32)) return hipErrorInvalidValue;  // item ids are 32-bit
   // shard s: tiles s, s + S, ... (interleaved across the image, so every shard
@@ -674,8 +698,8 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
 }
 
 int64_t mk_max_batch(const DevFrame& fr) {
-  // item ids (tile, sample, pixel of the 8x8 tile) are 32-bit: tiles * batch * 64 < 2^32
-  const int64_t tiles = (int64_t)((fr.w + kMkTile - 1) / kMkTile) * ((fr.n_rows + kMkTile - 1) / kMkTile);
+  // item ids (tile, sample, pixel of the 64-pixel tile) are 32-bit: tiles * batch * 64 < 2^32
+  const int64_t tiles = mk_tiles(fr);
   const int64_t padded = (tiles + kMkShards - 1) / kMkShards * kMkShards;  // interleaved shards' virtual units
   return tiles > 0 ? ((1ll << 32) - 1) / (padded * 64) : 0;
 }
