@@ -15,9 +15,11 @@
 //     hit's material, into one of five lists with wave64 ballot + mbcnt (one
 //     atomic per wave and list): Lambertian, metal/isotropic, dielectric,
 //     constant-medium boundary, Perlin-textured surface;
-//   * PER-MATERIAL SHADE KERNELS: wf_shade_lambertian / wf_shade_glossy /
-//     wf_shade_dielectric each run one material's scatter (kernels.py:817-917)
-//     over their list, so a wave executes one material's code only;
+//   * PER-MATERIAL SHADING: one wf_shade launch walks the Lambertian, glossy
+//     and dielectric lists in turn, each padded to whole waves, so every wave
+//     runs one material's scatter (kernels.py:817-917) only (three separate
+//     launches lost 6 %: a launch costs ~7.5 us per pipe and iteration even
+//     when its list is empty);
 //     wf_medium does the constant-medium exit traversal (kernels.py:417) and
 //     free flight, and the Perlin-textured surfaces (three octaves of table
 //     gathers, kernels.py:1013-1015) after them;
@@ -38,7 +40,7 @@
 //     device-wide counter saturates near 88 returning atomics/us on MI355X
 //     (MI355X_MICROARCH.md, "dequeue") and was measured at 97 % wait cycles.
 //   * PIPES: the queue is split into 4 independent parts, each looping
-//     intersect -> shade (3 material kernels) -> medium on its own stream, so
+//     intersect -> shade -> medium on its own stream, so
 //     the drain at the end of one pipe's launch is filled by another's (+21 %
 //     over one pipe).
 //   * The host learns that a pipe has drained from a 4-byte live count read
