@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 7
+#define PTMI_ABI_VERSION 6
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -105,12 +105,9 @@ enum { PTMI_TRAV_STACK = 0, PTMI_TRAV_STACKLESS = 1 };
 
 /* One render request: camera + render state (fields.py:171-172) + the pixel
  * set this call owns. The pixel set is the window [x0,x0+w) x [y0,y0+h)
- * restricted to the rows of the bands band_offset owns (band_stride = 1:
- * every row). Band b = (row - y0) / band_rows; the bands go to the
- * band_stride owners in groups of band_stride, serpentine (ABI 7): in group
- * g = b / band_stride, position p = b % band_stride belongs to owner p if g is
- * even and to owner band_stride - 1 - p if g is odd. Multi-GPU tile sharding
- * uses band_stride = world size, band_offset = rank. */
+ * restricted to rows whose band ((row - y0) / band_rows) satisfies
+ * band % band_stride == band_offset (band_stride = 1: every row). Multi-GPU
+ * tile sharding uses band_stride = world size, band_offset = rank. */
 typedef struct ptmi_frame {
     ptmi_camera cam;
     float bg[3];

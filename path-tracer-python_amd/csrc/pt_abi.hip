@@ -159,7 +159,7 @@ static int to_dev_frame(const ptmi_frame* f, DevFrame& d) {
   d.traversal = f->traversal;
   int32_t n = 0;
   for (int32_t r = 0; r < f->h; ++r)
-    if (band_owner(r / f->band_rows, f->band_stride) == f->band_offset) ++n;
+    if ((r / f->band_rows) % f->band_stride == f->band_offset) ++n;
   d.n_rows = n;
   return PTMI_OK;
 }

@@ -76,24 +76,11 @@ __device__ __forceinline__ int32_t leaf_index(int32_t ref) { return ref & 0x01ff
 // material class of a leaf (PTMI_CLASS_*, include/ptmi.h), packed by the host
 __device__ __forceinline__ int32_t leaf_class(int32_t ref) { return (ref >> 25) & 7; }
 
-// Row bands of the window (band b = (row - y0) / band_rows) go to the
-// band_stride owners in groups of band_stride bands, serpentine: owner p takes
-// position p of even groups and position stride - 1 - p of odd ones, so every
-// owner's mean row is the same and a top-to-bottom cost gradient (sky above,
-// geometry below) does not load the last owner most (plain round-robin: 8
-// GPUs at 4-row bands, owner 7's rows 28 rows lower on average, 4 % slower).
-__host__ __device__ __forceinline__ int32_t band_owner(int32_t band, int32_t stride) {
-  const int32_t g = band / stride, p = band - g * stride;
-  return (g & 1) ? stride - 1 - p : p;
-}
-
-// Local row (0..n_rows-1) -> image row, or -1. The frame owns exactly one
-// band per group, so its local band is the group index.
+// Local row (0..n_rows-1) -> image row, or -1.
 __device__ __forceinline__ int32_t frame_row(const DevFrame& fr, int32_t lr) {
-  const int32_t g = lr / fr.band_rows;
-  const int32_t within = lr - g * fr.band_rows;
-  const int32_t pos = (g & 1) ? fr.band_stride - 1 - fr.band_offset : fr.band_offset;
-  const int32_t row = fr.y0 + (g * fr.band_stride + pos) * fr.band_rows + within;
+  int32_t band = lr / fr.band_rows;
+  int32_t within = lr - band * fr.band_rows;
+  int32_t row = fr.y0 + (band * fr.band_stride + fr.band_offset) * fr.band_rows + within;
   return (row < fr.y0 + fr.h) ? row : -1;
 }
 

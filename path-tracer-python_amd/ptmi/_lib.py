@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PTMI_LIB') or os.path.join(_HERE, '_lib', 'libptmi.so')  # PTMI_LIB: A/B builds
-ABI_VERSION = 7  # PTMI_ABI_VERSION of include/ptmi.h
+ABI_VERSION = 6  # PTMI_ABI_VERSION of include/ptmi.h
 MAX_IMAGES = 16
 NUM_COUNTERS = 5
 

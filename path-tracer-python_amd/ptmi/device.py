@@ -15,7 +15,6 @@ import numpy as np
 import torch
 
 from . import _lib
-from .distributed import band_owner
 from .scene_data import DeviceLayout, SceneArrays, camera_upload, pack_device
 
 
@@ -134,7 +133,7 @@ def make_frame(cam, bg, max_depth, seed, width, height, window=None, band=(1, 1,
 def frame_pixel_rows(frame):
     """Image rows owned by a frame (window + band filter), as the kernels see them."""
     rows = [frame.y0 + r for r in range(frame.h)
-            if band_owner(r // frame.band_rows, frame.band_stride) == frame.band_offset]
+            if (r // frame.band_rows) % frame.band_stride == frame.band_offset]
     return np.asarray(rows, np.int64)
 
 

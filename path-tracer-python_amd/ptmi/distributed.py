@@ -6,8 +6,7 @@ writes only accum[py, px]) and every path's random stream is keyed by
 (seed, pixel, sample) (include/ptmi_rng.h), so the render shards without any
 exchange during rendering. Two partitions:
 
-* ``tiles``: interleaved row bands (band_rows rows, serpentine over the
-  ranks: see band_owner)
+* ``tiles``: interleaved row bands (band_rows rows, round-robin over ranks)
   — every pixel is rendered entirely by one rank, so the gathered image is
   bit-identical to a 1-GPU render; one sum-reduce of the f32 accumulator
   (the other ranks' bands are zero) assembles it on the root.
@@ -21,18 +20,6 @@ CPU tests): W*H*3*4 bytes = 7.7 MB at 800x800, once per render.
 from __future__ import annotations
 
 from dataclasses import dataclass
-
-
-def band_owner(band, stride):
-    """Rank that owns row band ``band`` (0-based from the window top) of
-    ``stride`` ranks: groups of ``stride`` bands, serpentine — rank p takes
-    position p of even groups and position stride - 1 - p of odd ones — so
-    all ranks have the same mean row. With plain round-robin a cost gradient
-    down the image loads the last rank most: vol2 at 8 GPUs, 4-row bands,
-    rank 7 4 % slower than rank 0 (tools/shard_balance.py). The device twin
-    is band_owner / frame_row in csrc/pt_device.hpp (ptmi.h, ABI 7)."""
-    g, p = divmod(band, stride)
-    return stride - 1 - p if g % 2 else p
 
 
 @dataclass(frozen=True)
@@ -75,7 +62,7 @@ class Shard:
     def rows(self, height):
         """Image rows this rank owns (tiles) or all rows (samples)."""
         b, s, o = self.band()
-        return [r for r in range(height) if band_owner(r // b, s) == o]
+        return [r for r in range(height) if (r // b) % s == o]
 
 
 def reduce_accum(accum, dst=0, group=None):

@@ -142,29 +142,6 @@ def test_tile_bands_partition_rows(h, band_rows, world):
     assert sorted(rows) == list(range(h))
 
 
-@pytest.mark.parametrize('h,band_rows,world', [(800, 4, 8), (800, 8, 3), (225, 8, 8), (37, 4, 5), (2160, 8, 8)])
-def test_library_counts_the_same_band_rows(h, band_rows, world):
-    """The library's row count for a banded frame (seen through the staged
-    workspace size, no GPU needed) is the Python partition's."""
-    lib = _lib.load()
-    for r in range(world):
-        sh = Shard(r, world, 'tiles', band_rows)
-        f = make_frame(height=h, band=sh.band())
-        npix = f.w * len(sh.rows(h))
-        assert lib.ptmi_mk_workspace_bytes(C.byref(f), 4) == (npix * 48 + 255) // 256 * 256 + 2048
-
-
-def test_serpentine_bands_even_out_the_mean_row():
-    """Bands go to the ranks serpentine (ptmi.h, ABI 7): 800 rows in 4-row
-    bands over 8 ranks give every rank 100 rows with the same mean row
-    (round-robin: rank 7's 28 rows lower than rank 0's)."""
-    from ptmi.distributed import band_owner
-    assert [band_owner(b, 4) for b in range(12)] == [0, 1, 2, 3, 3, 2, 1, 0, 0, 1, 2, 3]
-    means = [np.mean(Shard(r, 8, 'tiles', 4).rows(800)) for r in range(8)]
-    assert max(means) - min(means) <= 4 * 8 / 25  # one unpaired group of 25
-    assert all(len(Shard(r, 8, 'tiles', 4).rows(800)) == 100 for r in range(8))
-
-
 def test_sample_shards_are_disjoint_and_complete():
     world, steps, sps = 4, 5, 3
     seen = []

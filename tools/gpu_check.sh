@@ -7,7 +7,3 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 tail -1 $O/dist2.json | cut -c 1-600
 timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { echo BENCH_FAIL; tail $O/bench_c2.err; exit 1; }
 tail -1 $O/bench_c2.json | cut -c 1-300
-for o in "" "--reverse"; do
-timeout -k 10 200 python tools/shard_balance.py --preset c2 --ranks 8 $o > $O/bal8$o.json 2>&1 || { echo BAL_FAIL; exit 1; }
-tail -1 $O/bal8$o.json | cut -c 1-600
-done

@@ -28,7 +28,6 @@ def main():
     p.add_argument('--ranks', type=int, default=8)
     p.add_argument('--repeat', type=int, default=2, help='timed rounds over all ranks (min per rank kept)')
     p.add_argument('--band-rows', type=int, default=0, help='force this band height (default: Shard.balanced)')
-    p.add_argument('--reverse', action='store_true', help='time the ranks last to first (order-effect check)')
     args, rest = p.parse_known_args()
     import torch
     import bench
@@ -56,9 +55,8 @@ def main():
         render(frames[r], shards[r].sample_range(0, sps)[0])
     torch.cuda.synchronize()
     times = [float('inf')] * args.ranks
-    order = list(range(args.ranks))[::-1] if args.reverse else list(range(args.ranks))
     for _ in range(args.repeat):
-        for r in order:
+        for r in range(args.ranks):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(a.steps):
@@ -71,7 +69,7 @@ def main():
     mean = sum(times) / len(times)
     print(json.dumps({
         'preset': a.preset, 'scene': a.scene, 'width': W, 'height': H, 'variant': a.variant,
-        'partition': a.shard, 'ranks': args.ranks, 'order': 'reverse' if args.reverse else 'forward', 'band_rows': shards[0].band()[0],
+        'partition': a.shard, 'ranks': args.ranks, 'band_rows': shards[0].band()[0],
         'steps': a.steps, 'spp_per_step': sps,
         'rank_rows': rows, 'rank_s': [round(t, 5) for t in times],
         'imbalance_max_over_mean': round(max(times) / mean, 4),
