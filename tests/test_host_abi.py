@@ -142,6 +142,18 @@ def test_tile_bands_partition_rows(h, band_rows, world):
     assert sorted(rows) == list(range(h))
 
 
+@pytest.mark.parametrize('h,band_rows,world', [(800, 4, 8), (800, 8, 3), (225, 8, 8), (37, 4, 5), (2160, 8, 8)])
+def test_library_counts_the_same_band_rows(h, band_rows, world):
+    """The library's row count for a banded frame (seen through the staged
+    workspace size, no GPU needed) is the Python partition's."""
+    lib = _lib.load()
+    for r in range(world):
+        sh = Shard(r, world, 'tiles', band_rows)
+        f = make_frame(height=h, band=sh.band())
+        npix = f.w * len(sh.rows(h))
+        assert lib.ptmi_mk_workspace_bytes(C.byref(f), 4) == (npix * 48 + 255) // 256 * 256 + 2048
+
+
 def test_sample_shards_are_disjoint_and_complete():
     world, steps, sps = 4, 5, 3
     seen = []
