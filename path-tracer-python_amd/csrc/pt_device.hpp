@@ -56,6 +56,7 @@ struct DevScene {
   const int32_t* __restrict__ perlin_perm;
   const float4* __restrict__ ref_nodes;  // reference-layout nodes (stackless traversal), 3 float4 each
   int32_t n_nodes;                       // all BVH nodes
+  int32_t num_tris;                      // triangles (selects the leaf-deferring megakernel)
 };
 
 struct DevFrame {
@@ -410,7 +411,18 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // 80 B (profiles/r01/ab_node_layout.log). Two-level 256-B node packets (a
 // node's children and grandchildren, the near child expanded in the same
 // step) -20 to -43 % (profiles/r02/ab/ab_trav2_packets.log).
-template <int STACK, int SB = kBlock>
+//
+// DEFER > 0 (leaf deferral): a lane whose top entry is a live quad or
+// triangle test keeps it (no pop) while fewer than DEFER lanes of the wave
+// have such a test on top and some other lane has other work, so the
+// expensive leaf branch later runs for more lanes at once. Each lane still
+// pops its own entries in its own order: results are unchanged (GPU parity
+// and counters green). Used by the megakernel for scenes with triangles
+// (PTMI_MK_DEFER); A/B on MI355X, C4: threshold 8 / 12 / 16 / 24 +5 / +6 /
+// +3 / -5 %; triangles only at 12 / 20 -7 / -23 %; vol2 (spheres + quads, no
+// triangles) lost 2-6 % with it in round 2 (profiles/r02/ab/ab_leaf_defer.log,
+// profiles/r03/ab/ab_leaf_defer_mesh.log).
+template <int STACK, int SB = kBlock, int DEFER = 0>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
   // global address space: global_load, not flat_load (a laundered generic
@@ -422,6 +434,15 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   tr.sp -= kSlot;
   const pt_u2v ent = lds_load2(tr.sp);
   const int32_t ref = (int32_t)ent.x;
+  if constexpr (DEFER > 0) {
+    const bool dl = ref < 0 && leaf_type(ref) != kSphere && __uint_as_float(ent.y) <= tr.closest;
+    const unsigned long long md = pt_ballot(dl), mact = pt_ballot(true);
+    const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
+    if (md != 0ull && md != mact && nd < (uint32_t)DEFER && dl) {
+      tr.sp += kSlot;  // kept on top: popped in a later step
+      return;
+    }
+  }
 #if PTMI_PROBE
 #if PTMI_PROBE == 1
   atomicAdd(&g_probe[4], 1ull);                                                    // pops
@@ -543,7 +564,7 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, TravSL& tr, Stack
 }
 
 // One iteration of the reference's while loop (kernels.py:493-595).
-template <int STACK, int SB = kBlock>
+template <int STACK, int SB = kBlock, int DEFER = 0>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4*, TravSL& tr, Stack, pt_v3 o, pt_v3 d) {
   ++tr.it;
   const float4* nd = sc.ref_nodes + 3 * tr.node;
