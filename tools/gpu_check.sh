@@ -7,3 +7,5 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 tail -1 $O/dist2.json | cut -c 1-600
 timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { echo BENCH_FAIL; tail $O/bench_c2.err; exit 1; }
 tail -1 $O/bench_c2.json | cut -c 1-300
+timeout -k 10 300 python bench.py --preset c4 > $O/bench_c4.json 2> $O/bench_c4.err || { echo BENCH_FAIL; tail $O/bench_c4.err; exit 1; }
+tail -1 $O/bench_c4.json | cut -c 1-300
