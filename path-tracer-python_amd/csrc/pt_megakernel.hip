@@ -691,7 +691,10 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
   if (fr.traversal == PTMI_TRAV_STACKLESS)
     return launch_mk_trace<1, PTMI_TRAV_STACKLESS>(sc, fr, st, s_begin, nb, counters, stream);
 #if PTMI_MK_DEFER > 0
-  if (sc.num_tris > 0) {  // mesh scenes: the leaf-deferring kernels
+#ifndef PTMI_MK_DEFER_ALL
+#define PTMI_MK_DEFER_ALL 0  // A/B: the leaf-deferring kernels for every scene
+#endif
+  if (sc.num_tris > 0 || PTMI_MK_DEFER_ALL) {  // mesh scenes: the leaf-deferring kernels
     if (stack_needed <= PTMI_MK_STAGED_MIN_STACK)
       return launch_mk_trace<16, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
 #if PTMI_MK_EXACT_STACK
