@@ -56,7 +56,7 @@ struct DevScene {
   const int32_t* __restrict__ perlin_perm;
   const float4* __restrict__ ref_nodes;  // reference-layout nodes (stackless traversal), 3 float4 each
   int32_t n_nodes;                       // all BVH nodes
-  int32_t num_tris;                      // triangles (selects the leaf-deferring megakernel)
+  int32_t leaf_defer;                    // 1: every leaf is a quad or triangle (the leaf-deferring megakernel)
 };
 
 struct DevFrame {
@@ -417,11 +417,11 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // have such a test on top and some other lane has other work, so the
 // expensive leaf branch later runs for more lanes at once. Each lane still
 // pops its own entries in its own order: results are unchanged (GPU parity
-// and counters green). Used by the megakernel for scenes with triangles
-// (PTMI_MK_DEFER); A/B on MI355X, C4: threshold 8 / 12 / 16 / 24 +5 / +6 /
-// +3 / -5 %; triangles only at 12 / 20 -7 / -23 %; vol2 (spheres + quads, no
-// triangles) lost 2-6 % with it in round 2 (profiles/r02/ab/ab_leaf_defer.log,
-// profiles/r03/ab/ab_leaf_defer_mesh.log).
+// and counters green). Used by the megakernel for scenes without spheres
+// (PTMI_MK_DEFER); A/B on MI355X, C4 (quads + triangles): threshold 8 / 12 /
+// 16 / 24 +5 / +6 / +3 / -5 %, triangles only at 12 / 20 -7 / -23 %; at 12:
+// cornell_box +5 %, cornell_smoke +-0.5 %, vol2 (spheres + quads) -3 %
+// (profiles/r02/ab/ab_leaf_defer.log, profiles/r03/ab/ab_leaf_defer_mesh.log).
 template <int STACK, int SB = kBlock, int DEFER = 0>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {

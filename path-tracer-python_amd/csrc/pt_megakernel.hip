@@ -98,7 +98,8 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // shading round (C2 +1.6 %, C4 +2.3 %; profiles/r02/ab/ab_mk_one_begin.log).
 #ifndef PTMI_MK_DEFER
 // Leaf deferral (trav_step's DEFER, pt_device.hpp) in the staged kernels of
-// scenes with triangles, at this many lanes: C4 +6 % (0 = off).
+// scenes whose leaves are all quads and triangles, at this many lanes: C4 +6 %,
+// cornell_box +5 % (0 = off).
 #define PTMI_MK_DEFER 12
 #endif
 #ifndef PTMI_MK_MIN_WAVES
@@ -691,10 +692,7 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
   if (fr.traversal == PTMI_TRAV_STACKLESS)
     return launch_mk_trace<1, PTMI_TRAV_STACKLESS>(sc, fr, st, s_begin, nb, counters, stream);
 #if PTMI_MK_DEFER > 0
-#ifndef PTMI_MK_DEFER_ALL
-#define PTMI_MK_DEFER_ALL 0  // A/B: the leaf-deferring kernels for every scene
-#endif
-  if (sc.num_tris > 0 || PTMI_MK_DEFER_ALL) {  // mesh scenes: the leaf-deferring kernels
+  if (sc.leaf_defer) {  // scenes without spheres: the leaf-deferring kernels
     if (stack_needed <= PTMI_MK_STAGED_MIN_STACK)
       return launch_mk_trace<16, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
 #if PTMI_MK_EXACT_STACK
