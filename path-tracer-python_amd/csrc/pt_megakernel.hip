@@ -68,6 +68,13 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_SHADE_AT_DEEP PTMI_MK_SHADE_AT
 #endif
 
+#ifndef PTMI_MK_SHADE_AT_DEFER
+// ... and for the leaf-deferring kernels (PTMI_MK_DEFER). A/B on MI355X with
+// deferral at 12: 24 vs 16, C4 +1.4 %, cornell_box +2 %; 20: +0.9 / +2.4 %;
+// (24, deferral 16) +2 / +0.4 % (profiles/r03/ab/ab_leaf_defer_mesh.log).
+#define PTMI_MK_SHADE_AT_DEFER 24
+#endif
+
 #ifndef PTMI_MK_STEP_UNROLL
 #define PTMI_MK_STEP_UNROLL 3  // A/B with SHADE_AT 16: 3 pops per header pass +1.9 % C2, +2.6 % C4 (2: +1.5 %, 4: +1.6 %)
 #endif
@@ -329,7 +336,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      if (nbusy <= (uint32_t)(STACK > 16 ? PTMI_MK_SHADE_AT_DEEP : PTMI_MK_SHADE_AT) && pt_ballot(trav && !tr.busy()) != 0ull) break;
+      if (nbusy <= (uint32_t)(DEFER > 0 ? PTMI_MK_SHADE_AT_DEFER : STACK > 16 ? PTMI_MK_SHADE_AT_DEEP : PTMI_MK_SHADE_AT) &&
+          pt_ballot(trav && !tr.busy()) != 0ull)
+        break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
