@@ -64,10 +64,9 @@ PRESETS = {
 ALGO_BYTES = {
     # read o,d (24 B) + write hit t,ref (8 B) per ray
     'wf_intersect': ('rays', 32),
-    # read ray record 48 B + hit 8 B, write next record 48 B
-    'wf_shade': ('rays', 104),
-    # read medium index 4 B + hit 8 B + ray 48 B, write next record 48 B
-    'wf_medium': ('medium rays', 108),
+    # per traced segment that continues: read list index 4 B + hit 8 B + ray
+    # record 48 B, write the next record 48 B (surface shading and medium alike)
+    'wf_scatter': ('rays', 108),
     # SURVEY.md §8d graded figure per sample, B_sample = 44 + 24 + 128*S with
     # S = measured segments/sample: the bytes the reference's stage pipeline
     # must move for one camera path (the megakernel keeps them in registers)
@@ -360,7 +359,7 @@ def main():
     unit_name, unit_bytes = ALGO_BYTES[dom]
     if unit_bytes is None:
         unit_bytes = b_sample
-    units = {'wf_intersect': cnt['segments'], 'wf_shade': cnt['segments'], 'wf_medium': cnt['medium'],
+    units = {'wf_intersect': cnt['segments'], 'wf_scatter': cnt['segments'],
              'megakernel': samples_rank,
              'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
              'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]

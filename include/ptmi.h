@@ -246,8 +246,10 @@ int ptmi_bvh_build_sah(const float *spheres, int32_t ns, const float *quads, int
  * ptmi_prof_start pre-creates events for max_launches launches; render calls
  * then record around every kernel; ptmi_prof_stop synchronises, returns the
  * summed milliseconds and launch counts per kernel kind
- * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 wf_shade, 4 wf_medium,
- * 5 wf_resolve, 6 mk_resolve} and disables timing. One profiling session
+ * {0 megakernel, 1 wf_generate, 2 wf_intersect, 3 (retired: the separate
+ * wf_shade of earlier versions, no launches), 4 wf_scatter (shading and the
+ * medium exit search, one launch per wavefront iteration), 5 wf_resolve,
+ * 6 mk_resolve} and disables timing. One profiling session
  * per process; render calls from several host threads may record into it
  * (each launch owns its event pair; the session is mutex-guarded). */
 #define PTMI_PROF_KINDS 7

@@ -93,7 +93,7 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // A/B, not kept (profiles/): Perlin-textured hits held until 4 or 8 of a wave
 // are ready, -1 to -1.5 % (r01/ab_mk_hold_noise.log); non-temporal staging
 // stores, +-0.3 % (r02/ab/ab_nontemporal.log); one random_unit_vector site per
-// shading round (the wavefront's wf_medium keeps it), C2 -1.1 %
+// shading round (the wavefront's wf_scatter keeps it), C2 -1.1 %
 // (r02/ab/ab_one_scatter.log); the unit fetch's shard loop kept rolled,
 // -0.6 to -1.1 % (r02/ab/ab_mk_fetch_rolled.log).
 // Staged mode keeps the path's staging slot, computed when its item is bound,

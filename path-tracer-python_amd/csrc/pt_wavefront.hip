@@ -15,14 +15,14 @@
 //     hit's material, into one of five lists with wave64 ballot + mbcnt (one
 //     atomic per wave and list): Lambertian, metal/isotropic, dielectric,
 //     constant-medium boundary, Perlin-textured surface;
-//   * PER-MATERIAL SHADING: one wf_shade launch walks the Lambertian, glossy
-//     and dielectric lists in turn, each padded to whole waves, so every wave
-//     runs one material's scatter (kernels.py:817-917) only (three separate
-//     launches lost 6 %: a launch costs ~7.5 us per pipe and iteration even
-//     when its list is empty);
-//     wf_medium does the constant-medium exit traversal (kernels.py:417) and
-//     free flight, and the Perlin-textured surfaces (three octaves of table
-//     gathers, kernels.py:1013-1015) after them;
+//   * PER-MATERIAL SHADING: one wf_scatter launch walks the medium, Perlin,
+//     Lambertian, glossy and dielectric lists in turn, each padded to whole
+//     waves, so every wave runs one list's code only: the constant-medium
+//     exit traversal (kernels.py:417) and free flight, the Perlin-textured
+//     surfaces (three octaves of table gathers, kernels.py:1013-1015), or one
+//     material's scatter (kernels.py:817-917). Separate launches per material
+//     lost 6 %, separate shading and medium launches 5 %: a launch costs
+//     ~7.5 us per pipe and iteration even when its lists are empty;
 //   * WORK POOL, IN-PLACE SLOTS: the reference pushes one sample of every
 //     pixel through max_depth bounce-synchronous waves (renderer.py:305-334)
 //     and compacts survivors into a next queue with one atomic per ray, so
@@ -40,7 +40,7 @@
 //     device-wide counter saturates near 88 returning atomics/us on MI355X
 //     (MI355X_MICROARCH.md, "dequeue") and was measured at 97 % wait cycles.
 //   * PIPES: the queue is split into 4 independent parts, each looping
-//     intersect -> shade -> medium on its own stream, so
+//     intersect -> scatter on its own stream, so
 //     the drain at the end of one pipe's launch is filled by another's (+21 %
 //     over one pipe).
 //   * The host learns that a pipe has drained from a 4-byte live count read
@@ -84,7 +84,7 @@ struct Queue {
   float4* c;  // thr.xyz, meta (bits)
 };
 
-// Closest-hit lists (wf_intersect fills them, the shading kernels drain them).
+// Closest-hit lists (wf_intersect fills them, wf_scatter drains them).
 // Each list holds kShards segments of medseg slot indices; the medium and
 // Perlin lists share one array, the Perlin one filling its segments from the top
 // (a slot is in at most one list, so together they never exceed a segment).
@@ -93,7 +93,7 @@ enum : int32_t { kListLambertian = 0, kListGlossy = 1, kListDielectric = 2, kLis
 
 struct WfBufs {
   Queue q;
-  float2* hit;        // t, ref (bits); ref kMissRef = miss
+  float2* hit;        // t, leaf ref (bits) of a traced slot's closest hit (misses end in wf_intersect)
   int32_t* lists;     // 4 arrays of capacity indices: Lambertian, glossy, dielectric, medium + Perlin
   float* staging;     // [batch][npix][3] path colours
   int32_t* ctl;       // this pipe's counters, one per 256-B line (see ctl_*)
@@ -112,8 +112,6 @@ struct WfBufs {
   FastDiv by_per, by_nsq, by_sqx;  // item decode: / (64 * csamp), / nsq, / sq_x
 };
 
-constexpr int32_t kMissRef = 0x7fffffff;
-
 // Pipes: the queue is split into PTMI_WF_PIPES independent halves, each
 // driven through its own intersect/shade/medium loop on its own stream, so
 // one pipe's kernels fill the drain at the end of the other's. They share the
@@ -128,8 +126,8 @@ constexpr int32_t kPipes = PTMI_WF_PIPES;
 // 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 81
 // lines: live slots (read by the host), and two sets (by iteration parity)
 // of one count per list and shard. wf_intersect of iteration k appends to set
-// k & 1 and the shading kernels read it; wf_medium, the iteration's last
-// kernel, zeroes set (k + 1) & 1 for the next iteration's wf_intersect.
+// k & 1 and wf_scatter reads it and zeroes set (k + 1) & 1 for the next
+// iteration's wf_intersect.
 constexpr int32_t kLine = 64;
 constexpr int32_t kPipeLines = 1 + 2 * kLists * 8;
 constexpr int32_t kCtlWords = (8 + kPipeLines * kPipes) * kLine;
@@ -397,7 +395,7 @@ __device__ __forceinline__ void end_path(const DevFrame& fr, const WfBufs& wb, i
 // leaf codes by the host, so a hit's list is known without a material load.
 // Surface hits whose scatter evaluates Perlin turbulence (a noise texture on
 // a Lambertian or isotropic material, kernels.py:1013-1015) have their own
-// class, shaded by wf_medium: a marble lane would otherwise put three octaves
+// class, with its own list in wf_scatter: a marble lane would otherwise put three octaves
 // of table round trips into every Lambertian wave that holds it.
 static_assert(PTMI_CLASS_LAMBERTIAN == kListLambertian && PTMI_CLASS_GLOSSY == kListGlossy &&
                   PTMI_CLASS_DIELECTRIC == kListDielectric && PTMI_CLASS_MEDIUM == kListMedium &&
@@ -526,7 +524,7 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, const WfBuf
   return true;
 }
 
-// Per-lane tail of the shading kernels for a path that ended: stage its
+// Per-lane tail of wf_scatter for a path that ended: stage its
 // colour (0 unless it ended on an emissive boundary fallback; emissive
 // surface hits end in wf_intersect) and mark the slot as waiting for work (the
 // next wf_intersect hands it the next item).
@@ -560,152 +558,149 @@ __device__ __forceinline__ int32_t list_counts(const WfBufs& wb, int32_t par, in
   return n;
 }
 
-// shade_and_scatter (kernels.py:1289-1399) for the surface hits, one
-// material per wave: the work index runs over the Lambertian, glossy and
-// dielectric lists in turn, each padded to a multiple of 64 entries, so every
-// wave shades one list — Lambertian (scatter kernels.py:829-849 + its
-// texture, :924-1017), dielectric (:876-903) or glossy (metal :853-871,
-// isotropic :905-915, and anything else scatter() receives) — and runs that
-// material's code only. The surface hit point and normal are the reference's
-// (kernels.py:1359-1364); every draw keeps the reference's order.
-#ifndef PTMI_WF_SHADE_MIN_WAVES
-#define PTMI_WF_SHADE_MIN_WAVES 5  // 96 VGPRs, no spills: A/B C3 +0.8 %; 6 waves (48 B spills) -2.7 % (profiles/r02/ab/ab_wf_occupancy.log)
-#endif
-__global__ __launch_bounds__(kWfBlock, PTMI_WF_SHADE_MIN_WAVES) void wf_shade(DevScene sc, DevFrame fr, WfBufs wb,
-                                                    int32_t par, unsigned long long* __restrict__ counters) {
-  __shared__ unsigned int tally[3];
-  int32_t cnt[3][kShards], span[3];
-#pragma unroll
-  for (int l = 0; l < 3; ++l) span[l] = (list_counts(wb, par, l, cnt[l]) + 63) & ~63;
-  const int32_t n = span[0] + span[1] + span[2];
-  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
-  uint32_t n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
-    // wave-uniform list and offset of this wave's 64 entries
-    int32_t j = base + (int32_t)threadIdx.x, list = 0;
-    if (j >= span[0]) {
-      j -= span[0];
-      list = 1;
-      if (j >= span[1]) {
-        j -= span[1];
-        list = 2;
-      }
-    }
-    const int32_t nl = list == 0 ? cnt[0][0] + cnt[0][1] + cnt[0][2] + cnt[0][3] + cnt[0][4] + cnt[0][5] + cnt[0][6] + cnt[0][7]
-                     : list == 1 ? cnt[1][0] + cnt[1][1] + cnt[1][2] + cnt[1][3] + cnt[1][4] + cnt[1][5] + cnt[1][6] + cnt[1][7]
-                                 : cnt[2][0] + cnt[2][1] + cnt[2][2] + cnt[2][3] + cnt[2][4] + cnt[2][5] + cnt[2][6] + cnt[2][7];
-    if (j >= nl) continue;  // the list's padding
-    const int32_t i = list == 0 ? list_entry(wb, kListLambertian, cnt[0], j)
-                    : list == 1 ? list_entry(wb, kListGlossy, cnt[1], j) : list_entry(wb, kListDielectric, cnt[2], j);
-    const float2 h = h_load(wb.hit + i);
-    const int32_t ref = __float_as_int(h.y);
-    const Ray ray = load_ray(wb.q, i);
-    const Mat m = load_mat(sc, mat_index(sc, ref));
-    Item it = decode_item(fr, wb, ray.item);
-    Rng r{path_key(fr, wb, it), ray.ctr};
-    const pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
-    const pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
-    pt_v3 sdir = pt_v3f(0.0f, 0.0f, 0.0f), att = pt_v3f(1.0f, 1.0f, 1.0f);
-    bool sc_ok = true;
-    if (list == kListLambertian) {  // kernels.py:829-849
-      att = eval_texture(sc, ref, m, hp);
-      sdir = random_cosine_direction(nrm, r);
-    } else if (list == kListDielectric) {  // kernels.py:876-903
-      sdir = scatter_dielectric(m, ray.d, nrm, r);
-    } else {
-      sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
-    }
-    const bool go = scatter_epilogue(fr, wb, i, sc_ok, hp, sdir, att, ray, r, ends);
-    if (!go) {
-      finish_ended(fr, wb, i, ray, emitted(m));
-      ++n_ended;
-    }
+// One entry i of the Lambertian, glossy or dielectric list (`list`,
+// wave-uniform): shade_and_scatter for a surface hit (kernels.py:1359-1399).
+__device__ __forceinline__ void shade_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t list,
+                                            int32_t i, uint32_t& n_ended, uint32_t (&ends)[2]) {
+  const float2 h = h_load(wb.hit + i);
+  const int32_t ref = __float_as_int(h.y);
+  const Ray ray = load_ray(wb.q, i);
+  const Mat m = load_mat(sc, mat_index(sc, ref));
+  Item it = decode_item(fr, wb, ray.item);
+  Rng r{path_key(fr, wb, it), ray.ctr};
+  const pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
+  const pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
+  pt_v3 sdir = pt_v3f(0.0f, 0.0f, 0.0f), att = pt_v3f(1.0f, 1.0f, 1.0f);
+  bool sc_ok = true;
+  if (list == kListLambertian) {  // kernels.py:829-849
+    att = eval_texture(sc, ref, m, hp);
+    sdir = random_cosine_direction(nrm, r);
+  } else if (list == kListDielectric) {  // kernels.py:876-903
+    sdir = scatter_dielectric(m, ray.d, nrm, r);
+  } else {
+    sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
   }
-  if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, tally, counters + 2);
+  const bool go = scatter_epilogue(fr, wb, i, sc_ok, hp, sdir, att, ray, r, ends);
+  if (!go) {
+    finish_ended(fr, wb, i, ray, emitted(m));
+    ++n_ended;
+  }
 }
 
-// Constant-medium rays: exit traversal + free flight (apply_constant_medium,
-// kernels.py:365-450) and the volume branch of shade_and_scatter
-// (kernels.py:1326-1357); then the Perlin-textured surfaces. Work index j runs
-// over the medium list's shard segments, then the Perlin list's.
-template <int STACK, int TRAV = PTMI_TRAV_STACK>
-#ifndef PTMI_WF_MEDIUM_MIN_WAVES
-#define PTMI_WF_MEDIUM_MIN_WAVES 4  // <= 128 VGPRs: with the Perlin list it needs 131 otherwise (3 waves/SIMD)
+// One entry i of the constant-medium list (exit traversal + free flight,
+// apply_constant_medium kernels.py:365-450, and the volume branch of
+// shade_and_scatter, kernels.py:1326-1357) or, is_noise, of the Perlin list.
+template <int STACK, int TRAV>
+__device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, Stack st,
+                                             int32_t i, bool is_noise, uint32_t& n_ended, uint32_t (&ends)[2]) {
+  bool ended = false, go = false;
+  pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
+  const float2 h = h_load(wb.hit + i);
+  const int32_t ref = __float_as_int(h.y);
+  const Ray ray = load_ray(wb.q, i);
+  float te = 0.0f;
+  int32_t rex = 0;
+  bool hx = false;
+  if (!is_noise)  // the exit search from t_entry + 1e-4 (kernels.py:417-419)
+    hx = traverse<STACK, kWfBlock, TRAV>(sc, ray.o, ray.d, h.x + 0.0001f, kTMax, st, te, rex);
+  const Mat m = load_mat(sc, mat_index(sc, ref));
+  Item it = decode_item(fr, wb, ray.item);
+  Rng r{path_key(fr, wb, it), ray.ctr};
+  bool surface = is_noise, scattered = false, passthrough = false;
+  int32_t ruv = kRuvNone;
+  pt_v3 hp, nrm, sdir, att;
+  if (!is_noise) {
+    float t_exit;
+    pt_v3 mp;
+    if (medium_step(hx, te, h.x, m.m3.w, ray.o, ray.d, r, mp, t_exit)) {
+      hp = mp;
+      att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
+      ruv = kRuvMedium;
+      scattered = true;
+    } else if (t_exit > 0.0f) {  // passthrough: same depth, next wave (kernels.py:1342-1350)
+      passthrough = true;
+      int32_t wave = (int32_t)((ray.meta >> 8) & 0xffu);
+      if (wave + 1 >= fr.max_depth) {
+        ++ends[1];  // Q14: no wave left for the passthrough
+      } else {
+        float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
+        store_ray_v(wb.q, i, pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t)), ray.d, ray.thr, ray.item, r.n,
+                    ray.meta + (1u << 8));
+        go = true;
+      }
+    } else {  // fallback: the boundary as a surface (kernels.py:1352-1357)
+      surface = true;
+    }
+  }
+  if (surface) {  // one scatter site: Perlin-textured hits and boundary fallbacks
+    hp = pt_add(ray.o, pt_scale(ray.d, h.x));
+    nrm = hit_normal(sc, ref, hp, ray.d);
+    emit = emitted(m);
+    ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, scattered);
+  }
+  if (ruv != kRuvNone) {  // one random_unit_vector site
+    const pt_v3 v = random_unit_vector(r);
+    if (ruv == kRuvMedium) sdir = v;
+    else scattered = scatter_end(sc, ruv, ref, m, hp, nrm, v, sdir, att);
+  }
+  if (!passthrough) go = scatter_epilogue(fr, wb, i, scattered, hp, sdir, att, ray, r, ends);
+  ended = !go;
+  if (ended) finish_ended(fr, wb, i, ray, emit);
+  n_ended += ended ? 1u : 0u;
+}
+
+// shade_and_scatter (kernels.py:1289-1399) and the constant-medium exit
+// search and free flight (apply_constant_medium, kernels.py:365-450) in one
+// launch per iteration and pipe: the work index runs over the medium, Perlin,
+// Lambertian, glossy and dielectric lists in turn (the traversing medium
+// waves first: they are the longest), each padded to whole waves, so every
+// wave runs one list's code only — Lambertian (scatter kernels.py:829-849 +
+// its texture, :924-1017), dielectric (:876-903), glossy (metal :853-871,
+// isotropic :905-915, and anything else scatter() receives), the medium
+// (:1326-1357) or the Perlin-textured surfaces. A/B on MI355X against a
+// shading launch and a medium launch per iteration (parity-identical): C3
+// +4.8 %, mesh fog -1.8 % (the shading waves run at the medium's 4
+// waves/SIMD; profiles/r03/ab/ab_wf_fused.log). The surface hit point and
+// normal are the reference's (kernels.py:1359-1364); every draw keeps the
+// reference's order.
+#ifndef PTMI_WF_SCATTER_MIN_WAVES
+#define PTMI_WF_SCATTER_MIN_WAVES 4  // <= 128 VGPRs (116, the medium exit traversal's Perlin path needs them)
 #endif
-__global__ __launch_bounds__(kWfBlock, PTMI_WF_MEDIUM_MIN_WAVES) void wf_medium(DevScene sc, DevFrame fr, WfBufs wb,
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
+__global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatter(DevScene sc, DevFrame fr, WfBufs wb,
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
-  int32_t cnt[kShards], cntn[kShards];  // per-shard medium / Perlin counts (wave-uniform)
-  const int32_t n = list_counts(wb, par, kListMedium, cnt);
-  const int32_t nn = list_counts(wb, par, kListNoise, cntn);
+  constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
+  int32_t cnt[kLists][kShards], num[kLists], span[kLists];  // wave-uniform
+  int32_t n = 0;
+#pragma unroll
+  for (int l = 0; l < kLists; ++l) {
+    num[l] = list_counts(wb, par, kOrder[l], cnt[l]);
+    span[l] = (num[l] + 63) & ~63;
+    n += span[l];
+  }
   if (blockIdx.x < kShards && threadIdx.x < kLists)  // the next iteration's lists start empty
     *ctl_list(wb, par ^ 1, (int32_t)threadIdx.x, (int32_t)blockIdx.x) = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && counters && n > 0) atomicAdd(counters + 1, (unsigned long long)n);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && counters && num[0] > 0) atomicAdd(counters + 1, (unsigned long long)num[0]);
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n + nn; base += stride) {
-    const int32_t j = base + (int32_t)threadIdx.x;
-    bool ended = false, go = false;
-    pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
+    // wave-uniform list of this wave's 64 entries
+    int32_t j = base + (int32_t)threadIdx.x, l = 0;
+#pragma unroll
+    for (int k = 0; k + 1 < kLists; ++k)
+      if (l == k && j >= span[k]) {
+        j -= span[k];
+        l = k + 1;
+      }
     int32_t i = -1;
-    const bool is_noise = j >= n && j < n + nn;
-    if (j < n) i = list_entry(wb, kListMedium, cnt, j);
-    else if (is_noise) i = list_entry(wb, kListNoise, cntn, j - n);
-    if (i >= 0) {
-      const float2 h = h_load(wb.hit + i);
-      const int32_t ref = __float_as_int(h.y);
-      const Ray ray = load_ray(wb.q, i);
-      float te = 0.0f;
-      int32_t rex = 0;
-      bool hx = false;
-      if (!is_noise)  // the exit search from t_entry + 1e-4 (kernels.py:417-419)
-        hx = traverse<STACK, kWfBlock, TRAV>(sc, ray.o, ray.d, h.x + 0.0001f, kTMax, st, te, rex);
-      const Mat m = load_mat(sc, mat_index(sc, ref));
-      Item it = decode_item(fr, wb, ray.item);
-      Rng r{path_key(fr, wb, it), ray.ctr};
-      bool surface = is_noise, scattered = false, passthrough = false;
-      int32_t ruv = kRuvNone;
-      pt_v3 hp, nrm, sdir, att;
-      if (!is_noise) {
-        float t_exit;
-        pt_v3 mp;
-        if (medium_step(hx, te, h.x, m.m3.w, ray.o, ray.d, r, mp, t_exit)) {
-          hp = mp;
-          att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
-          ruv = kRuvMedium;
-          scattered = true;
-        } else if (t_exit > 0.0f) {  // passthrough: same depth, next wave (kernels.py:1342-1350)
-          passthrough = true;
-          int32_t wave = (int32_t)((ray.meta >> 8) & 0xffu);
-          if (wave + 1 >= fr.max_depth) {
-            ++ends[1];  // Q14: no wave left for the passthrough
-          } else {
-            float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
-            store_ray_v(wb.q, i, pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t)), ray.d, ray.thr, ray.item, r.n,
-                        ray.meta + (1u << 8));
-            go = true;
-          }
-        } else {  // fallback: the boundary as a surface (kernels.py:1352-1357)
-          surface = true;
-        }
-      }
-      if (surface) {  // one scatter site: Perlin-textured hits and boundary fallbacks
-        hp = pt_add(ray.o, pt_scale(ray.d, h.x));
-        nrm = hit_normal(sc, ref, hp, ray.d);
-        emit = emitted(m);
-        ruv = scatter_begin(sc, ref, m, ray.d, hp, nrm, r, sdir, att, scattered);
-      }
-      if (ruv != kRuvNone) {  // one random_unit_vector site
-        const pt_v3 v = random_unit_vector(r);
-        if (ruv == kRuvMedium) sdir = v;
-        else scattered = scatter_end(sc, ruv, ref, m, hp, nrm, v, sdir, att);
-      }
-      if (!passthrough) go = scatter_epilogue(fr, wb, i, scattered, hp, sdir, att, ray, r, ends);
-      ended = !go;
-      if (ended) finish_ended(fr, wb, i, ray, emit);
-    }
-    n_ended += ended ? 1u : 0u;
+#pragma unroll
+    for (int k = 0; k < kLists; ++k)
+      if (l == k && j < num[k]) i = list_entry(wb, kOrder[k], cnt[k], j);
+    if (i < 0) continue;  // the list's padding
+    if (l < 2) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, l == 1, n_ended, ends);
+    else shade_entry(sc, fr, wb, kOrder[l], i, n_ended, ends);  // kOrder[l] for l = 2, 3, 4: selects
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
 }
@@ -784,7 +779,7 @@ Layout layout(int32_t npix, int32_t batch) {
 static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must be a multiple of the shard count");
 
 // One batch: generate on the caller's stream, fork the pipes, run each pipe's
-// intersect -> shade -> medium loop on its own stream until its slots have all
+// intersect -> scatter loop on its own stream until its slots have all
 // retired, join, resolve.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs* wbs, float* accum, int32_t batch,
@@ -833,12 +828,9 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
         const int ps_i = prof_begin(kProfWfIntersect, st[p]);
         hipLaunchKernelGGL((wf_intersect<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
         prof_end(ps_i, st[p]);
-        const int ps_s = prof_begin(kProfWfShade, st[p]);
-        hipLaunchKernelGGL(wf_shade, dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
+        const int ps_s = prof_begin(kProfWfScatter, st[p]);
+        hipLaunchKernelGGL((wf_scatter<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
         prof_end(ps_s, st[p]);
-        const int ps_m = prof_begin(kProfWfMedium, st[p]);
-        hipLaunchKernelGGL((wf_medium<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
-        prof_end(ps_m, st[p]);
       }
     }
     it += n;

@@ -45,7 +45,7 @@ def test_every_preset_has_measured_traffic(preset, kernel):
 
 
 def test_algorithmic_bytes_cover_every_kernel_kind():
-    assert set(bench.ALGO_BYTES) >= {'megakernel', 'wf_intersect', 'wf_shade', 'wf_medium', 'wf_generate',
+    assert set(bench.ALGO_BYTES) >= {'megakernel', 'wf_intersect', 'wf_scatter', 'wf_generate',
                                      'wf_resolve', 'mk_resolve'}
 
 
