@@ -119,7 +119,6 @@ static int to_dev_scene(const ptmi_scene_view* s, DevScene& d) {
   d.perlin_perm = s->perlin_perm;
   d.ref_nodes = (const float4*)s->ref_nodes;
   d.n_nodes = s->num_bvh_nodes;
-  d.leaf_defer = s->num_spheres == 0 && s->num_quads + s->num_triangles > 0;
   return PTMI_OK;
 }
 

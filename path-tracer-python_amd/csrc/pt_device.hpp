@@ -56,7 +56,6 @@ struct DevScene {
   const int32_t* __restrict__ perlin_perm;
   const float4* __restrict__ ref_nodes;  // reference-layout nodes (stackless traversal), 3 float4 each
   int32_t n_nodes;                       // all BVH nodes
-  int32_t leaf_defer;                    // 1: every leaf is a quad or triangle (the leaf-deferring megakernel)
 };
 
 struct DevFrame {
@@ -412,16 +411,18 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // node's children and grandchildren, the near child expanded in the same
 // step) -20 to -43 % (profiles/r02/ab/ab_trav2_packets.log).
 //
-// DEFER > 0 (leaf deferral): a lane whose top entry is a live quad or
-// triangle test keeps it (no pop) while fewer than DEFER lanes of the wave
-// have such a test on top and some other lane has other work, so the
-// expensive leaf branch later runs for more lanes at once. Each lane still
-// pops its own entries in its own order: results are unchanged (GPU parity
-// and counters green). Used by the megakernel for scenes without spheres
-// (PTMI_MK_DEFER); A/B on MI355X, C4 (quads + triangles): threshold 8 / 12 /
-// 16 / 24 +5 / +6 / +3 / -5 %, triangles only at 12 / 20 -7 / -23 %; at 12:
-// cornell_box +5 %, cornell_smoke +-0.5 %, vol2 (spheres + quads) -3 %
-// (profiles/r02/ab/ab_leaf_defer.log, profiles/r03/ab/ab_leaf_defer_mesh.log).
+// DEFER > 0 (leaf deferral): a lane whose top entry is a live leaf test
+// (sphere, quad or triangle) keeps it (no pop) while fewer than DEFER lanes of
+// the wave have a leaf test on top and some other lane has other work (a node
+// step), so the leaf branches later run for more lanes at once. Each lane
+// still pops its own entries in its own order: results are unchanged (GPU
+// parity and counters green). The megakernel uses it (PTMI_MK_DEFER); A/B on
+// MI355X against no deferral, with its shading threshold: every leaf at 12
+// lanes, shading at <= 24 busy lanes: C2 +7.5 %, C5 +6.3 %, C4 +8 %; at 16 /
+// 20 lanes +7 / +6 % (C2); quads and triangles only: C4 +6 %, C2 -3 %;
+// spheres only at 4 / 8: C2 +0.5 %; triangles only -7 to -23 % (C4)
+// (profiles/r03/ab/ab_leaf_defer.log; round 2's per-class forms,
+// profiles/r02/ab/ab_leaf_defer.log).
 template <int STACK, int SB = kBlock, int DEFER = 0>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
@@ -435,7 +436,7 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const pt_u2v ent = lds_load2(tr.sp);
   const int32_t ref = (int32_t)ent.x;
   if constexpr (DEFER > 0) {
-    const bool dl = ref < 0 && leaf_type(ref) != kSphere && __uint_as_float(ent.y) <= tr.closest;
+    const bool dl = ref < 0 && __uint_as_float(ent.y) <= tr.closest;
     const unsigned long long md = pt_ballot(dl), mact = pt_ballot(true);
     const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
     if (md != 0ull && md != mact && nd < (uint32_t)DEFER && dl) {
@@ -630,6 +631,8 @@ struct TravOf<PTMI_TRAV_STACKLESS> {
 #ifndef PTMI_TRAV_UNROLL
 #define PTMI_TRAV_UNROLL 3  // pops per loop test in traverse() (wavefront kernels; A/B: 3 +0.5 % C3 / mesh fog, 2 +0.3 %)
 #endif
+// No leaf deferral here: in the wavefront's one-ray-per-lane traversals it
+// lost 3-12 % (DEFER 8 / 12 / 20, C3 and mesh fog; profiles/r03/ab/ab_leaf_defer.log).
 template <int STACK, int SB = kBlock, int TRAV = PTMI_TRAV_STACK>
 __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
                                          float& t_out, int32_t& ref_out) {

@@ -57,22 +57,11 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 }
 
 #ifndef PTMI_MK_SHADE_AT
-#define PTMI_MK_SHADE_AT 16  // shade once at most this many lanes are still mid-traversal (A/B with the
-                             // traversal priority: 12 ~ 16 > 10 > 8 >> 4; without it 8 > 16 > 24 > 0;
-                             // with 3 pops per header pass 16 > 12)
-#endif
-
-#ifndef PTMI_MK_SHADE_AT_DEEP
-// The threshold for kernels with more than 16 stack slots (deep BVHs such as
-// C4's torus, whose traversals are longer and more uneven): A/B knob.
-#define PTMI_MK_SHADE_AT_DEEP PTMI_MK_SHADE_AT
-#endif
-
-#ifndef PTMI_MK_SHADE_AT_DEFER
-// ... and for the leaf-deferring kernels (PTMI_MK_DEFER). A/B on MI355X with
-// deferral at 12: 24 vs 16, C4 +1.4 %, cornell_box +2 %; 20: +0.9 / +2.4 %;
-// (24, deferral 16) +2 / +0.4 % (profiles/r03/ab/ab_leaf_defer_mesh.log).
-#define PTMI_MK_SHADE_AT_DEFER 24
+// Shade once at most this many lanes are still mid-traversal. With leaf
+// deferral (PTMI_MK_DEFER 12): 24 > 20 > 16 (C2 +1.7 % / +1 %; C4 +1.4 %);
+// before it 12 ~ 16 > 10 > 8 >> 4 with the traversal priority, 8 > 16 > 24 > 0
+// without (profiles/r03/ab/ab_leaf_defer.log, profiles/r01/ab_prio_shade_at.log).
+#define PTMI_MK_SHADE_AT 24
 #endif
 
 #ifndef PTMI_MK_STEP_UNROLL
@@ -104,9 +93,8 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // instead of two divergent copies (3 divisions + the root slab) in one
 // shading round (C2 +1.6 %, C4 +2.3 %; profiles/r02/ab/ab_mk_one_begin.log).
 #ifndef PTMI_MK_DEFER
-// Leaf deferral (trav_step's DEFER, pt_device.hpp) in the staged kernels of
-// scenes whose leaves are all quads and triangles, at this many lanes: C4 +6 %,
-// cornell_box +5 % (0 = off).
+// Leaf deferral (trav_step's DEFER, pt_device.hpp) at this many lanes: C2
+// +7.5 %, C5 +6.3 %, C4 +8 % with the shading threshold at 24 (0 = off).
 #define PTMI_MK_DEFER 12
 #endif
 #ifndef PTMI_MK_MIN_WAVES
@@ -209,7 +197,7 @@ static int64_t mk_tiles(const DevFrame& fr, int32_t* tx_out = nullptr) {
   return tx * ty;
 }
 
-template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK, int DEFER = 0>
+template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves/SIMD the LDS stack allows: 160 KiB / (STACK * 8 B * 256) blocks per CU
 // (16 -> 5, 20 -> 4, 24 -> 3, 32 -> 2), and the VGPR budget of that many
 // waves (96 at 5, 128 at 4).
@@ -336,9 +324,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      if (nbusy <= (uint32_t)(DEFER > 0 ? PTMI_MK_SHADE_AT_DEFER : STACK > 16 ? PTMI_MK_SHADE_AT_DEEP : PTMI_MK_SHADE_AT) &&
-          pt_ballot(trav && !tr.busy()) != 0ull)
-        break;
+      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -346,7 +332,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // and shading test sit on every wave's serial chain)
 #pragma unroll
       for (int u = 0; u < PTMI_MK_STEP_UNROLL; ++u)
-        if (tr.busy()) trav_step<STACK, kMkBlock, DEFER>(sc, nodes, tr, st, ps.o, ps.dir);
+        if (tr.busy()) trav_step<STACK, kMkBlock, PTMI_MK_DEFER>(sc, nodes, tr, st, ps.o, ps.dir);
 #if PTMI_PROBE == 2
       ++pr_steps;
       pr_sph += pt_ballot(tr.probe & 1) ? 1 : 0;
@@ -646,7 +632,7 @@ size_t mk_workspace_bytes(int32_t npix, int32_t batch) {  // staging + the shard
 // The megakernel of one staged batch: every (sample, pixel) colour of the
 // batch into staging[sample][pixel]; the accumulator is not touched (the
 // resolve is launch_stage_resolve, on the caller's schedule).
-template <int STACK, int TRAV = PTMI_TRAV_STACK, int DEFER = 0>
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float* staging, int32_t s_begin,
                                   int32_t nb, unsigned long long* counters, hipStream_t stream) {
   float* accum = nullptr;  // staged kernels write staging only
@@ -656,7 +642,7 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   hipError_t e0 = hipGetDevice(&dev);
   if (e0 == hipSuccess) e0 = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e0 == hipSuccess)
-    e0 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk_render_kernel<STACK, true, TRAV, DEFER>, kMkBlock, 0);
+    e0 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk_render_kernel<STACK, true, TRAV>, kMkBlock, 0);
   if (e0 != hipSuccess) return e0;
   MkWork wk;
   wk.ctl = (int32_t*)((char*)staging + mk_staging_bytes(fr.w * fr.n_rows, nb));
@@ -689,7 +675,7 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   wk.tail_div = (int32_t)(tdiv > 1 ? tdiv : 1);
   (void)hipMemsetAsync(wk.ctl, 0, 256 * kMkShards, stream);
   const int pslot = prof_begin(kProfMk, stream);
-  hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV, DEFER>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
+  hipLaunchKernelGGL((mk_render_kernel<STACK, true, TRAV>), dim3((unsigned)waves), dim3(kMkBlock), 0, stream,
                      sc, fr, accum, s_begin, nb, nb, staging, counters, wk);
   prof_end(pslot, stream);
   return hipGetLastError();
@@ -700,18 +686,6 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
   float* st = (float*)ws;
   if (fr.traversal == PTMI_TRAV_STACKLESS)
     return launch_mk_trace<1, PTMI_TRAV_STACKLESS>(sc, fr, st, s_begin, nb, counters, stream);
-#if PTMI_MK_DEFER > 0
-  if (sc.leaf_defer) {  // scenes without spheres: the leaf-deferring kernels
-    if (stack_needed <= PTMI_MK_STAGED_MIN_STACK)
-      return launch_mk_trace<16, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
-#if PTMI_MK_EXACT_STACK
-    if (stack_needed == 17) return launch_mk_trace<17, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
-    if (stack_needed == 18) return launch_mk_trace<18, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
-    if (stack_needed == 19) return launch_mk_trace<19, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
-#endif
-    if (stack_needed <= 20) return launch_mk_trace<20, PTMI_TRAV_STACK, PTMI_MK_DEFER>(sc, fr, st, s_begin, nb, counters, stream);
-  }
-#endif
   if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) return launch_mk_trace<16>(sc, fr, st, s_begin, nb, counters, stream);
 #if PTMI_MK_EXACT_STACK
   if (stack_needed == 17) return launch_mk_trace<17>(sc, fr, st, s_begin, nb, counters, stream);
