@@ -27,12 +27,18 @@ def main():
     W, H = run.W, run.H
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
     out = {}
-    for spp in (64, 32, 16, 8):
+    for spp in [int(x) for x in os.environ.get('CALL_SIZE_SPP', '64,32,16,8').split(',')]:
         out[f'full_{spp}spp'] = round(rate(run.integ, run.frame, acc, W * H, spp), 1)
-    for ranks, band in ((8, 4), (8, 8), (4, 8), (2, 8)):
+    shards = os.environ.get('CALL_SIZE_SHARDS', '8:4,8:8,4:8,2:8')
+    for ranks, band in [tuple(int(v) for v in x.split(':')) for x in shards.split(',') if x]:
         sh = Shard(0, ranks, 'tiles', band)
         fr = device.make_frame(run.cam, run.bg, 50, 0, W, H, band=sh.band())
         out[f'rank0_of_{ranks}_band{band}_64spp'] = round(rate(run.integ, fr, acc, W * len(sh.rows(H)), 64), 1)
+    if os.environ.get('CALL_SIZE_SHARDS') is not None:
+        out['lib'] = os.path.basename(os.environ.get('PTMI_LIB', 'libptmi.so'))
+        out['depth'] = os.environ.get('PTMI_OVERLAP_DEPTH', 'auto')
+        print(json.dumps(out))
+        return
     # a contiguous block of rows (no interleave) of the same size as one 8-rank shard
     fr = device.make_frame(run.cam, run.bg, 50, 0, W, H, window=(0, 352, W, 100))
     out['rows352_451_64spp'] = round(rate(run.integ, fr, acc, W * 100, 64), 1)
