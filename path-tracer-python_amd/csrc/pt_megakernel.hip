@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #if PTMI_PROBE == 2
   // wave-level probe (diagnostic build): shader cycles in the traversal-step
   // loop and in shading/refill; wave steps and the branches they ran
-  uint64_t pr_trav = 0, pr_shade = 0, pr_steps = 0, pr_sph = 0, pr_oth = 0, pr_node = 0;
+  uint64_t pr_trav = 0, pr_shade = 0, pr_steps = 0, pr_sph = 0, pr_oth = 0, pr_node = 0, pr_both = 0, pr_busy = 0;
   uint64_t pr_t = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
@@ -338,6 +338,8 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       pr_sph += pt_ballot(tr.probe & 1) ? 1 : 0;
       pr_oth += pt_ballot(tr.probe & 2) ? 1 : 0;
       pr_node += pt_ballot(tr.probe & 4) ? 1 : 0;
+      pr_both += (pt_ballot(tr.probe & 1) && pt_ballot(tr.probe & 2)) ? 1 : 0;
+      pr_busy += nbusy;
 #endif
     }
 #if PTMI_PROBE == 2
@@ -538,6 +540,8 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     atomicAdd(&g_probe[11], pr_sph);
     atomicAdd(&g_probe[12], pr_oth);
     atomicAdd(&g_probe[13], pr_node);
+    atomicAdd(&g_probe[14], pr_both);
+    atomicAdd(&g_probe[15], pr_busy);
   }
 #endif
   if (!STAGED && ap) {

@@ -31,7 +31,7 @@ torch.cuda.synchronize()
 lib.ptmi_probe_read(out, 1)
 c = integ.read_counters()
 n, u, steps, lanes, pops, culled, lsph, lother = list(out)[:8]
-cyc_trav, cyc_shade, wsteps, wsph, woth, wnode = list(out)[8:14]
+cyc_trav, cyc_shade, wsteps, wsph, woth, wnode, wboth, wbusy = list(out)[8:16]
 print(json.dumps({'scene': scene, 'spp': spp, 'node_visits': n, 'uniform_visit_frac': u / max(1, n),
                   'simd_eff_node_steps': lanes / max(1, 64 * steps), 'node_visits_per_traversal':
                   n / max(1, c['segments'] + c['medium']), 'pops_per_traversal': pops / max(1, c['segments'] + c['medium']),
@@ -40,5 +40,6 @@ print(json.dumps({'scene': scene, 'spp': spp, 'node_visits': n, 'uniform_visit_f
                   'probe2': {'cycles_trav_frac': cyc_trav / max(1, cyc_trav + cyc_shade), 'wave_steps_per_sample':
                              wsteps / max(1, c['paths']), 'sphere_step_frac': wsph / max(1, wsteps),
                              'quadtri_step_frac': woth / max(1, wsteps), 'node_step_frac': wnode / max(1, wsteps),
+                             'sphere_and_quadtri_step_frac': wboth / max(1, wsteps), 'busy_lanes_per_step': wbusy / max(1, wsteps),
                              'cycles_per_wave_step': cyc_trav / max(1, wsteps),
                              'shade_cycles_per_sample': cyc_shade / max(1, c['paths'])}, **c}))
