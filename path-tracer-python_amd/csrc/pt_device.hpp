@@ -317,8 +317,18 @@ __device__ __forceinline__ pt_f2 operator+(pt_f2 a, pt_f2 b) { return pt_f2{a.x 
 __device__ __forceinline__ pt_f2 operator-(pt_f2 a, pt_f2 b) { return pt_f2{a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ pt_f2 operator*(pt_f2 a, pt_f2 b) { return pt_f2{a.x * b.x, a.y * b.y}; }
 
+// A thread's traversal stack: slot k at slot0[k * SB] (SB = threads per
+// block) in LDS for k < LDS (a kernel template argument); a kernel whose LDS
+// holds fewer slots than the stack needs (LDS < STACK: wf_intersect, where
+// LDS sets the occupancy) keeps the deeper slots in global memory, slot k at
+// byte spill_off + (k - LDS) * spill_stride of spill (slot-major over the
+// grid's threads, so a wave's accesses are coalesced). Deep entries are rare:
+// the pops and pushes of the top LDS slots take the LDS path.
 struct Stack {
-  uint2* slot0;  // &lds[tid]; slot k at slot0[k * SB] (SB = threads per block)
+  uint2* slot0;              // &lds[tid]
+  char* spill = nullptr;     // global spill slots (LDS < STACK only)
+  uint32_t spill_off = 0;    // this thread's byte offset in a spill slot row
+  uint32_t spill_stride = 0; // bytes between a thread's consecutive spill slots
 };
 
 // LDS accesses by 32-bit byte address (a stack pointer kept as the address of
@@ -332,6 +342,36 @@ __device__ __forceinline__ void lds_store2(uint32_t a, uint32_t x, uint32_t y) {
   pt_lds_u32* q = (pt_lds_u32*)(uintptr_t)a;
   q[0] = x;
   q[1] = y;
+}
+
+// Stack slot access by LDS-style address a = slot0 + k * kSlot, for a stack
+// of LDS slots in LDS and the rest spilled (LDS < STACK); lim = the address
+// of slot LDS. With LDS == STACK these are the plain LDS accesses.
+typedef __attribute__((address_space(1))) pt_u2v pt_glb_u2v;
+template <int STACK, int LDS, int SB>
+__device__ __forceinline__ pt_u2v stack_load(const Stack& st, uint32_t lim, uint32_t a) {
+  if constexpr (LDS >= STACK) {
+    return lds_load2(a);
+  } else {
+    if (a < lim) return lds_load2(a);
+    constexpr int kShift = __builtin_ctz(SB * 8);
+    const uint32_t off = st.spill_off + ((a - lim) >> kShift) * st.spill_stride;
+    return *(const pt_glb_u2v*)((const __attribute__((address_space(1))) char*)st.spill + off);
+  }
+}
+template <int STACK, int LDS, int SB>
+__device__ __forceinline__ void stack_store(const Stack& st, uint32_t lim, uint32_t a, uint32_t x, uint32_t y) {
+  if constexpr (LDS >= STACK) {
+    lds_store2(a, x, y);
+  } else {
+    if (a < lim) {
+      lds_store2(a, x, y);
+    } else {
+      constexpr int kShift = __builtin_ctz(SB * 8);
+      const uint32_t off = st.spill_off + ((a - lim) >> kShift) * st.spill_stride;
+      *(pt_glb_u2v*)((__attribute__((address_space(1))) char*)st.spill + off) = pt_u2v{x, y};
+    }
+  }
 }
 
 // Lane mask of a predicate (v_cmp straight into an SGPR pair; __ballot's int
@@ -423,7 +463,7 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, Trav& tr, Stack s
 // spheres only at 4 / 8: C2 +0.5 %; triangles only -7 to -23 % (C4)
 // (profiles/r03/ab/ab_leaf_defer.log; round 2's per-class forms,
 // profiles/r02/ab/ab_leaf_defer.log).
-template <int STACK, int SB = kBlock, int DEFER = 0>
+template <int STACK, int SB = kBlock, int DEFER = 0, int LDS = STACK>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node_base, Trav& tr, Stack st, pt_v3 o,
                                           pt_v3 d) {
   // global address space: global_load, not flat_load (a laundered generic
@@ -432,8 +472,9 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   typedef const __attribute__((address_space(1))) pt_f4 gf4;
   gf4* nodes = (gf4*)node_base;
   constexpr uint32_t kSlot = SB * 8;  // bytes between a lane's consecutive slots
+  const uint32_t lim = tr.sp0 + (uint32_t)LDS * kSlot;  // address of the first spilled slot (LDS < STACK)
   tr.sp -= kSlot;
-  const pt_u2v ent = lds_load2(tr.sp);
+  const pt_u2v ent = stack_load<STACK, LDS, SB>(st, lim, tr.sp);
   const int32_t ref = (int32_t)ent.x;
   if constexpr (DEFER > 0) {
     const bool dl = ref < 0 && __uint_as_float(ent.y) <= tr.closest;
@@ -514,8 +555,8 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const unsigned long long mln = pt_ballot(ln), mh0 = pt_ballot(h0), mh1 = pt_ballot(h1);
   const bool up0 = __builtin_amdgcn_inverse_ballot_w64((mln & mh1) | (~mln & ~mh0));
   const uint32_t lo = tr.sp, hi = tr.sp + kSlot;
-  lds_store2(up0 ? hi : lo, __float_as_uint(R.x), __float_as_uint(E0));
-  lds_store2(up0 ? lo : hi, __float_as_uint(R.y), __float_as_uint(E1));
+  stack_store<STACK, LDS, SB>(st, lim, up0 ? hi : lo, __float_as_uint(R.x), __float_as_uint(E0));
+  stack_store<STACK, LDS, SB>(st, lim, up0 ? lo : hi, __float_as_uint(R.y), __float_as_uint(E1));
   tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
 }
 
@@ -565,7 +606,7 @@ __device__ __forceinline__ void trav_begin(const DevScene& sc, TravSL& tr, Stack
 }
 
 // One iteration of the reference's while loop (kernels.py:493-595).
-template <int STACK, int SB = kBlock, int DEFER = 0>
+template <int STACK, int SB = kBlock, int DEFER = 0, int LDS = STACK>
 __device__ __forceinline__ void trav_step(const DevScene& sc, const float4*, TravSL& tr, Stack, pt_v3 o, pt_v3 d) {
   ++tr.it;
   const float4* nd = sc.ref_nodes + 3 * tr.node;
@@ -633,15 +674,15 @@ struct TravOf<PTMI_TRAV_STACKLESS> {
 #endif
 // No leaf deferral here: in the wavefront's one-ray-per-lane traversals it
 // lost 3-12 % (DEFER 8 / 12 / 20, C3 and mesh fog; profiles/r03/ab/ab_leaf_defer.log).
-template <int STACK, int SB = kBlock, int TRAV = PTMI_TRAV_STACK>
+template <int STACK, int SB = kBlock, int TRAV = PTMI_TRAV_STACK, int LDS = STACK>
 __device__ __forceinline__ bool traverse(const DevScene& sc, pt_v3 o, pt_v3 d, float tmin, float tmax, Stack st,
                                          float& t_out, int32_t& ref_out) {
   typename TravOf<TRAV>::T tr;
-  trav_begin<STACK, SB>(sc, tr, st, d, o, tmin, tmax);
+  trav_begin<STACK, SB>(sc, tr, st, d, o, tmin, tmax);  // the root: slot 0, in LDS
   while (tr.busy()) {
 #pragma unroll
     for (int u = 0; u < PTMI_TRAV_UNROLL; ++u)
-      if (u == 0 || tr.busy()) trav_step<STACK, SB>(sc, sc.nodes, tr, st, o, d);
+      if (u == 0 || tr.busy()) trav_step<STACK, SB, 0, LDS>(sc, sc.nodes, tr, st, o, d);
   }
   t_out = tr.closest;
   ref_out = tr.best;

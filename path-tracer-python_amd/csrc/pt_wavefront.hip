@@ -75,6 +75,32 @@ constexpr int kShards = 8;
                            // C3 +1.2 %, mesh fog +1.7 %; 64: C3 -6 %, mesh fog +2.3 %; profiles/r02/ab/ab_wf_block.log)
 #endif
 constexpr int kWfBlock = PTMI_WF_BLOCK;
+#ifndef PTMI_WF_ISECT_LDS
+// Stack slots wf_intersect keeps in LDS when its stack is deeper than 16
+// slots; the deeper slots spill to global memory (Stack, pt_device.hpp). Its
+// LDS stacks set its occupancy: the 20-slot kernel (leaf depth 16-19, e.g.
+// the mesh-fog torus) fits 4 waves/SIMD with all slots in LDS, 7 with 11
+// (67 VGPRs). A/B on MI355X, parity-identical (also with 3 LDS slots, where
+// most pushes spill): mesh fog +2.2 %; for the 16-slot kernel (vol2, C3: 5
+// waves/SIMD) 7 waves gained nothing (-1.5 %; 6 waves -2.5 %; larger pipe
+// grids -1 to -5 %), so it keeps all 16 in LDS
+// (profiles/r03/ab/ab_wf_spill.log). A 16-slot wf_intersect padded down to 4
+// waves/SIMD loses 8 % (3 waves: 18 %).
+#define PTMI_WF_ISECT_LDS 11
+#endif
+#ifndef PTMI_WF_SPILL_MAX_STACK
+#define PTMI_WF_SPILL_MAX_STACK 20  // kernels of 17 to this many stack slots spill; deeper ones keep them all in LDS
+#endif
+constexpr int kSpillSlots = PTMI_WF_SPILL_MAX_STACK > PTMI_WF_ISECT_LDS ? PTMI_WF_SPILL_MAX_STACK - PTMI_WF_ISECT_LDS : 0;
+template <int STACK, int TRAV>
+constexpr int isect_lds() {
+  return (TRAV == PTMI_TRAV_STACK && STACK > 16 && STACK <= PTMI_WF_SPILL_MAX_STACK && PTMI_WF_ISECT_LDS < STACK)
+             ? PTMI_WF_ISECT_LDS
+             : STACK;
+}
+#ifndef PTMI_WF_MAX_BLOCKS
+#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together; A/B: 4096 -1.5 %, 8192 -3.5 % (C3)
+#endif
 constexpr uint32_t kDead = 0xffffffffu;     // item of a retired slot
 constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (assigned in wf_intersect)
 
@@ -97,6 +123,7 @@ struct WfBufs {
   int32_t* lists;     // 4 arrays of capacity indices: Lambertian, glossy, dielectric, medium + Perlin
   float* staging;     // [batch][npix][3] path colours
   int32_t* ctl;       // this pipe's counters, one per 256-B line (see ctl_*)
+  char* spill;        // this pipe's spilled stack slots of wf_intersect (kSpillSlots rows of its grid's threads)
   int32_t* next;      // next-unit counters shared by the pipes, one per 256-B line
   int32_t capacity;   // queue slots (multiple of kShards * kWfBlock)
   int32_t medseg;     // slots per shard
@@ -408,9 +435,10 @@ static_assert(PTMI_CLASS_LAMBERTIAN == kListLambertian && PTMI_CLASS_GLOSSY == k
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
-  __shared__ uint2 lds_stack[STACK * kWfBlock];
+  constexpr int LDS = isect_lds<STACK, TRAV>();
+  __shared__ uint2 lds_stack[LDS * kWfBlock];
   const int tid = threadIdx.x;
-  Stack st{lds_stack + tid};
+  Stack st{lds_stack + tid, wb.spill, (uint32_t)(blockIdx.x * kWfBlock + tid) * 8u, gridDim.x * kWfBlock * 8u};
   const Queue q = wb.q;
   const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
@@ -432,7 +460,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
       }
       float t;
       int32_t ref;
-      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
+      const bool hit = traverse<STACK, kWfBlock, TRAV, LDS>(sc, o, d, kTMin, kTMax, st, t, ref);
       if (hit) {
         list = leaf_class(ref);
         h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
@@ -750,8 +778,9 @@ constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
 struct Layout {
   int32_t capacity, medseg;
-  size_t q, hit, lists, grp, staging, ctl, total;
+  size_t q, hit, lists, grp, staging, spill, ctl, total;
 };
+constexpr size_t kSpillPipeBytes = (size_t)kSpillSlots * (PTMI_WF_MAX_BLOCKS / kPipes) * kWfBlock * 8;
 
 Layout layout(int32_t npix, int32_t batch) {
   Layout L;
@@ -767,15 +796,13 @@ Layout layout(int32_t npix, int32_t batch) {
   L.lists = L.hit + sizeof(float2) * c;
   L.grp = (L.lists + 4 * sizeof(int32_t) * c + 15) & ~(size_t)15;
   L.staging = (L.grp + sizeof(int2) * (c / 64) + 15) & ~(size_t)15;
-  L.ctl = (L.staging + 3 * sizeof(float) * (size_t)items + 255) & ~(size_t)255;
+  L.spill = (L.staging + 3 * sizeof(float) * (size_t)items + 255) & ~(size_t)255;
+  L.ctl = L.spill + kPipes * kSpillPipeBytes;
   L.total = L.ctl + kCtlWords * sizeof(int32_t);
   return L;
 }
 }  // namespace
 
-#ifndef PTMI_WF_MAX_BLOCKS
-#define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together; A/B: 4096 -1.5 %, 8192 -3.5 % (C3)
-#endif
 static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must be a multiple of the shard count");
 
 // One batch: generate on the caller's stream, fork the pipes, run each pipe's
@@ -921,6 +948,7 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
       wb.staging = (float*)(base + L.staging);
       wb.next = (int32_t*)(base + L.ctl);
       wb.ctl = wb.next + (8 + p * kPipeLines) * kLine;
+      wb.spill = base + L.spill + p * kSpillPipeBytes;
       wb.capacity = (int32_t)cp;
       wb.medseg = L.medseg;
       wb.npix = npix;
