@@ -692,7 +692,10 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
 // normal are the reference's (kernels.py:1359-1364); every draw keeps the
 // reference's order.
 #ifndef PTMI_WF_SCATTER_MIN_WAVES
-#define PTMI_WF_SCATTER_MIN_WAVES 4  // <= 128 VGPRs (116, the medium exit traversal's Perlin path needs them)
+// 5 waves/SIMD: <= 96 VGPRs (the 16-slot kernel: 96, 72 B/lane of scratch, against 116 VGPRs and 52 B at 4
+// waves). A/B on MI355X, parity-identical: C3 +2.1 %, mesh fog +3 % (profiles/r03/ab/ab_wf_scatter_waves.log).
+// Kernels of more than 16 stack slots stay at 4 (their 20+ KB LDS stacks allow no more).
+#define PTMI_WF_SCATTER_MIN_WAVES 5
 #endif
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatter(DevScene sc, DevFrame fr, WfBufs wb,
