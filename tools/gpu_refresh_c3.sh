@@ -1,5 +1,5 @@
 #!/bin/bash
-# C3 evidence refresh after the fused wf_scatter (not product): bench line, rocprofv3 kernel trace + stats
+# C3 evidence refresh (not product; round 3: after the fused wf_scatter, then its 5-wave build): bench line, rocprofv3 kernel trace + stats
 # of the C3 bench command, the two traffic PMC passes, the wf_intersect VALU/latency passes.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
