@@ -68,6 +68,8 @@ def load():
                                       P, C.POINTER(OrStats)]
         lib.or_math_probe.argtypes = [C.c_int, P, P, P, C.c_int]
         lib.or_rng_probe.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, P, P]
+        lib.or_func_probe.argtypes = [C.POINTER(OrScene), C.c_int, P, P, C.c_int]
+        lib.or_func_probe.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -188,3 +190,22 @@ def rng_probe(seed, pixel, sample, n):
     key = np.zeros(1, np.uint32)
     load().or_rng_probe(seed, pixel, sample, n, _ptr(out), _ptr(key))
     return out, int(key[0])
+
+
+# or_func_probe: function -> (id, input record length, output record length)
+FUNCS = {'perlin_noise': (0, 3, 1), 'perlin_turb': (1, 4, 1), 'sphere_uv': (2, 6, 2), 'reflect': (3, 6, 3),
+         'refract': (4, 7, 3), 'reflectance': (5, 2, 1), 'hit_sphere': (6, 12, 2), 'hit_quad': (7, 24, 2),
+         'hit_triangle': (8, 20, 2)}
+
+
+def func_probe(oscene, fn, records):
+    """One kernels.py function of the oracle on (n, in_len) f32 input records
+    (layouts in pt_oracle.h, or_func_probe); the Perlin functions use
+    oscene's tables. Returns (n, out_len) f32."""
+    fid, n_in, n_out = FUNCS[fn]
+    x = np.ascontiguousarray(records, np.float32).reshape(-1, n_in)
+    out = np.zeros((x.shape[0], n_out), np.float32)
+    got = load().or_func_probe(C.byref(oscene.s), fid, _ptr(x), _ptr(out), x.shape[0])
+    if got != n_in:
+        raise RuntimeError(f'or_func_probe({fn}) expects {got} inputs per record')
+    return out

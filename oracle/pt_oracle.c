@@ -78,9 +78,13 @@ static float perlin_noise(const or_scene *sc, pt_v3 p) {    /* kernels.py:110-15
     float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
     float u = p.x - fx, v = p.y - fy, w = p.z - fz;
     int32_t i = pt_f2i(fx), j = pt_f2i(fy), k = pt_f2i(fz);
+#ifndef OR_NEGATIVE_CONTROL_NO_HERMITE
     float uu = u * u * (3.0f - 2.0f * u);
     float vv = v * v * (3.0f - 2.0f * v);
     float ww = w * w * (3.0f - 2.0f * w);
+#else  /* tests/test_functions.py negative control only: a deliberately wrong Perlin */
+    float uu = u, vv = v, ww = w;
+#endif
     float accum = 0.0f;
     for (int di = 0; di < 2; ++di)
         for (int dj = 0; dj < 2; ++dj)
@@ -694,4 +698,43 @@ void or_rng_probe(uint32_t seed, uint32_t pixel, uint32_t sample, int n, float *
     uint32_t key = pt_path_key(seed, pixel, sample);
     if (key_out) *key_out = key;
     for (int i = 0; i < n; ++i) out[i] = pt_rand(key, (uint32_t)i);
+}
+
+int or_func_probe(const or_scene *sc, int fn, const float *in, float *out, int n) {
+    static const int in_len[9] = {3, 4, 6, 6, 7, 2, 12, 24, 20};
+    static const int out_len[9] = {1, 1, 2, 3, 3, 1, 2, 2, 2};
+    if (fn < 0 || fn > 8) return 0;
+    for (int i = 0; i < n; ++i) {
+        const float *x = in + (size_t)i * in_len[fn];
+        float *y = out + (size_t)i * out_len[fn];
+        pt_v3 a = pt_v3f(x[0], x[1], x[2]);
+        switch (fn) {
+        case 0: y[0] = perlin_noise(sc, a); break;
+        case 1: y[0] = perlin_turb(sc, a, (int)x[3]); break;
+        case 2: get_sphere_uv(a, pt_v3f(x[3], x[4], x[5]), &y[0], &y[1]); break;
+        case 3: { pt_v3 r = reflect(a, pt_v3f(x[3], x[4], x[5])); y[0] = r.x; y[1] = r.y; y[2] = r.z; } break;
+        case 4: { pt_v3 r = refract(a, pt_v3f(x[3], x[4], x[5]), x[6]); y[0] = r.x; y[1] = r.y; y[2] = r.z; } break;
+        case 5: y[0] = reflectance(x[0], x[1]); break;
+        default: {   /* one primitive in a scratch scene */
+            or_scene one = *sc;
+            hit_t h; int hit = 0;
+            const float *r = x + in_len[fn] - 8;   /* o[3], d[3], tmin, tmax */
+            pt_v3 o = pt_v3f(r[0], r[1], r[2]), d = pt_v3f(r[3], r[4], r[5]);
+            if (fn == 6) {
+                one.sphere_data = x;
+                hit = hit_sphere(&one, 0, o, d, r[6], r[7], &h);
+            } else if (fn == 7) {
+                one.quad_Q = x; one.quad_u = x + 3; one.quad_v = x + 6; one.quad_normal = x + 9;
+                one.quad_D = x + 12; one.quad_w = x + 13;
+                hit = hit_quad(&one, 0, o, d, r[6], r[7], &h);
+            } else {
+                one.tri_v0 = x; one.tri_e1 = x + 3; one.tri_e2 = x + 6; one.tri_normal = x + 9;
+                hit = hit_triangle(&one, 0, o, d, r[6], r[7], &h);
+            }
+            y[0] = (float)hit;
+            y[1] = hit ? h.t : 0.0f;
+        }
+        }
+    }
+    return in_len[fn];
 }

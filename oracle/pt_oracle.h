@@ -90,6 +90,19 @@ int or_trace_path(const or_scene *sc, const or_frame *fr, int variant, int px, i
                   float *color_out, or_stats *stats);
 /* math / rng probes for the known-answer tests */
 void or_math_probe(int fn, const float *x, const float *y, float *out, int n);
+/* per-function probes (known-answer tests against the reference's own Python,
+ * tests/golden/gen_functions.py). fn, input record -> output record:
+ *  0 perlin_noise    p[3] (sc's Perlin tables)           -> value
+ *  1 perlin_turb     p[3], depth                          -> value
+ *  2 get_sphere_uv   p[3], center[3]                      -> u, v
+ *  3 reflect         v[3], n[3]                           -> r[3]
+ *  4 refract         uv[3], n[3], eta                     -> r[3]
+ *  5 reflectance     cosine, ref_idx                      -> value
+ *  6 hit_sphere      c[3], r, o[3], d[3], tmin, tmax      -> hit, t
+ *  7 hit_quad        Q, u, v, normal[3], D, w[3], o, d, tmin, tmax -> hit, t
+ *  8 hit_triangle    v0, e1, e2, normal[3], o, d, tmin, tmax       -> hit, t
+ * Returns the input record length of fn (0 for an unknown fn). */
+int or_func_probe(const or_scene *sc, int fn, const float *in, float *out, int n);
 void or_rng_probe(uint32_t seed, uint32_t pixel, uint32_t sample, int n, float *out, uint32_t *key_out);
 #ifdef __cplusplus
 }

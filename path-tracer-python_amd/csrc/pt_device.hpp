@@ -23,8 +23,11 @@ constexpr float kRRMaxProb = 0.95f; // kernels.py:1051
 constexpr int kNumCounters = PTMI_NUM_COUNTERS;  // include/ptmi.h
 
 // n / d by one 64-bit multiply and shift: m = floor(2^(32+l) / d) + 1 with
-// 2^l >= d gives floor(n / d) exactly whenever n * d < 2^(32+l), which every
-// use below guarantees (work-item and unit ids < 2^32, divisors <= 2^l).
+// 2^l >= d (so m <= 2^33) gives floor(n / d) exactly for every n < 2^32 in
+// exact arithmetic; the 64-bit product n * m does not wrap while n < 2^31
+// (any n < 2^32 when d is a power of two, m = 2^32 + 1). Callers keep n below
+// 2^31: the megakernel divides unit ids (item >> 6), the wavefront padded work
+// item ids, bounded in wf_render.
 struct FastDiv {
   uint64_t m;
   uint32_t sh, d;

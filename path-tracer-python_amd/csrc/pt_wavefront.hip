@@ -916,9 +916,13 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
                      float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
                      hipStream_t stream) {
   const int32_t npix = fr.w * fr.n_rows;
-  // work items (sample, pixel) of a batch are 32-bit ids: at most 2^31 - 1
+  // work items (sample, pixel) of a batch are ids below 2^31 (FastDiv's
+  // range), padded ids included: 64 per 8x8 pixel square, and the batch's
+  // samples rounded up to whole chunks (wb.nunits below)
+  const int64_t sq_items = 64ll * ((fr.w + 7) / 8) * ((fr.n_rows + 7) / 8);
   int32_t batch = s_count;
-  if ((int64_t)npix * batch > 0x7fffffffll) batch = (int32_t)(0x7fffffffll / npix);
+  const int64_t max_batch = sq_items > 0 ? 0x7fffffffll / sq_items - (PTMI_WF_CHUNK_SAMPLES - 1) : 0;
+  if (batch > max_batch) batch = (int32_t)max_batch;
   if (batch < 1) return hipErrorInvalidValue;
   while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
   if (layout(npix, batch).total > ws_bytes) return hipErrorInvalidValue;

@@ -216,10 +216,10 @@ class Integrator:
         Ordering, whatever stream each call passes:
         * a trace into workspace half h waits for the resolve that last read
           half h (an event recorded on the stream that ran that resolve), and
-          for a counter reset issued since the previous trace
-          (reset_counters records it; the reset and read_counters in turn
-          wait for the traces still adding to the counters, whatever stream
-          they run on);
+          for every counter reset issued before it (reset_counters makes
+          every side stream wait on its event; the reset and read_counters in
+          turn wait for the traces still adding to the counters, whatever
+          stream they run on);
         * a resolve waits for its own trace and for the previous resolve, so
           the accumulator sees the batches in call order;
         * a trace does not wait for other work the caller queued after the
@@ -241,6 +241,9 @@ class Integrator:
                 D = self.OVERLAP_DEPTH_MAX
                 self._ov = {'streams': [torch.cuda.Stream(dev) for _ in range(D)], 'ws': [None] * D,
                             'k': 0, 'resolved': [None] * D, 'last_resolved': None, 'traced': [None] * D}
+                if self._reset_event is not None:  # a reset issued before the side streams existed
+                    for side in self._ov['streams']:
+                        side.wait_event(self._reset_event)
             ov = self._ov
             depth = int(os.environ.get('PTMI_OVERLAP_DEPTH', '0')) or \
                 (3 if npix * min(per, int(sample_count)) < self.OVERLAP_SMALL_CALL else 2)
@@ -264,9 +267,6 @@ class Integrator:
                     side.wait_event(fresh)
                 if ov['resolved'][h] is not None:
                     side.wait_event(ov['resolved'][h])
-                if self._reset_event is not None:
-                    side.wait_event(self._reset_event)
-                    self._reset_event = None
                 _lib.check(self.lib.ptmi_mk_trace_ws(C.byref(self.scene.view), C.byref(frame),
                                                      C.c_void_p(ws.data_ptr()), ws.numel() * 4,
                                                      int(sample_begin) + b, n, self._cnt(),
@@ -349,9 +349,16 @@ class Integrator:
             self._after_traces(s)
             with torch.cuda.stream(s):
                 self.counters.zero_()
-            # overlapped traces run on side streams: the next one waits for this reset
-            self._reset_event = torch.cuda.Event()
-            self._reset_event.record(s)
+            # overlapped traces run on side streams: every later trace, on any of
+            # them, waits for this reset (a multi-batch call rotates through the
+            # side streams, so waiting on the first one only is not enough)
+            ev = torch.cuda.Event()
+            ev.record(s)
+            ov = getattr(self, '_ov', None)
+            if ov is not None:
+                for side in ov['streams']:
+                    side.wait_event(ev)
+            self._reset_event = ev  # side streams created after this reset wait on it too
 
 
 def _check_accum(accum, frame, device=None):

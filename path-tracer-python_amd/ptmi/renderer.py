@@ -54,6 +54,9 @@ class MI355XRenderer:
         self.background_color = (0.70, 0.80, 1.00)
         self.seed = int(seed)
         self.use_stackless_traversal = USE_STACKLESS_TRAVERSAL
+        # integrator whose samples the accumulator holds (checkpoint state):
+        # render_sample() and render() use the megakernel
+        self._integrator_label = 'megakernel'
         # periodic checkpoints during render(): every `checkpoint_every` progress chunks
         self.checkpoint_path = None
         self.checkpoint_every = 1
@@ -111,6 +114,7 @@ class MI355XRenderer:
     def render_sample(self, sample: int):
         """One sample of every pixel (renderer.py:551-556): sample index
         ``sample`` of the counter-based stream, megakernel."""
+        self._integrator_label = 'megakernel'
         self.integrator.render_mk(self.frame, self.accum, int(sample), 1)
 
     def _run(self, render_fn, label, resume=False):
@@ -180,7 +184,7 @@ class MI355XRenderer:
         f = self.frame
         cam = np.array([list(f.cam.center), list(f.cam.pixel00), list(f.cam.delta_u), list(f.cam.delta_v),
                         list(f.cam.defocus_u), list(f.cam.defocus_v), [f.cam.defocus_angle, 0.0, 0.0]], np.float32)
-        return {'integrator': np.array(getattr(self, '_integrator_label', '')), 'seed': np.int64(f.seed), 'max_depth': np.int64(f.max_depth),
+        return {'integrator': np.array(self._integrator_label), 'seed': np.int64(f.seed), 'max_depth': np.int64(f.max_depth),
                 'background': np.array(list(f.bg), np.float32), 'traversal': np.int64(f.traversal),
                 'width': np.int64(f.width), 'height': np.int64(f.height), 'camera': cam,
                 'scene': np.array(h.hexdigest())}
@@ -250,14 +254,23 @@ class MI355XRenderer:
 
     def _get_rr_stats(self):
         """Russian-roulette statistics of the last render (renderer.py:481-500)
-        from the device counters: paths killed by RR (kernels.py:1145-1157), and
-        paths that reached the RR depth and survived to end another way (the
-        reference's rr_paths_survived). The reference's per-depth sums are not
-        kept (its atomics are disabled, kernels.py:1189-1202)."""
+        from the device counters.
+
+        Schema: the reference's keys, plus 'paths' and 'depth_cap'.
+        * 'killed': paths ended by RR (kernels.py:1145-1157), counted exactly.
+        * 'survived', 'total_rr_paths', 'avg_depth_killed',
+          'avg_depth_survived': None. The device does not count paths that
+          reached depth 3 unkilled, nor depth sums (kernels.py:1200-1202
+          define them). In the reference they are always 0, because the
+          atomics that would fill them are commented out (kernels.py:1189-1202).
+        * 'kill_rate': killed / all paths x 100. The reference divides by
+          killed + survived, which cannot be formed without 'survived'."""
         c = self.integrator.read_counters() or {}
         killed = c.get('rr', 0)
-        return {'killed': killed, 'paths': c.get('paths', 0), 'depth_cap': c.get('depth_cap', 0),
-                'kill_rate': 100.0 * killed / c['paths'] if c.get('paths') else 0.0}
+        return {'killed': killed, 'survived': None, 'total_rr_paths': None,
+                'kill_rate': 100.0 * killed / c['paths'] if c.get('paths') else 0.0,
+                'avg_depth_killed': None, 'avg_depth_survived': None,
+                'paths': c.get('paths', 0), 'depth_cap': c.get('depth_cap', 0)}
 
     def _get_average_depth(self):
         """Mean ray segments per path (renderer.py:473-479 reports the mean

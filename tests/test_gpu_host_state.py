@@ -215,6 +215,38 @@ def test_mk_overlapped_calls_on_changing_streams():
     assert integ.read_counters() == want_cnt
 
 
+def test_multi_batch_overlapped_call_after_unsynchronised_reset():
+    """A reset_counters(stream=...) with no synchronisation, followed by one
+    overlapped call split into several batches: every batch's trace (each on
+    its own side stream) runs after the reset, so the counters hold exactly
+    that call's paths (only the first trace used to wait)."""
+    import torch
+    from ptmi import device
+    sa, cam, bg = scene_inputs('vol2_final_scene', 800)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, cam['width'], cam['height'], (128, 256, 256, 128))
+    npix = 256 * 128
+    integ.STAGING_BYTES = 12 * npix * 2  # 2 samples per batch: a 6-sample call is 3 batches
+    ref = torch.zeros((cam['height'], cam['width'], 3), dtype=torch.float32, device='cuda')
+    integ.reset_counters()
+    integ.render_mk(fr, ref, 10, 6)
+    torch.cuda.synchronize()
+    want = integ.read_counters()
+    assert want['paths'] == 6 * npix
+    acc = torch.zeros_like(ref)
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for k in range(3):  # traces in flight on every side stream when the reset is queued
+        integ.render_mk(fr, acc, 2 * k, 2, overlap=True)
+    integ.reset_counters(stream=s)
+    acc2 = torch.zeros_like(ref)
+    integ.render_mk(fr, acc2, 10, 6, stream=s, overlap=True)
+    s.synchronize()
+    torch.cuda.synchronize()
+    assert integ.read_counters() == want
+    assert torch.equal(acc2, ref)
+
+
 def test_profiler_with_concurrent_megakernel_threads():
     """ptmi_prof_* with render calls from several host threads: every launch
     gets its own event pair (no mixed-up begin/end), so the launch counts are

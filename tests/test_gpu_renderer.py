@@ -136,6 +136,25 @@ def test_checkpoint_resume_is_bit_identical(tmp_path):
     assert os.path.exists(tmp_path / 'resumed.png')
 
 
+def test_checkpoint_after_render_sample_loop_resumes(tmp_path):
+    """A checkpoint saved after an InteractiveViewer-style render_sample()
+    loop records the megakernel, so render(resume=True) continues it and gets
+    the uninterrupted render bit for bit (the label was empty)."""
+    full = _smoke_renderer(6, str(tmp_path / 'full.png'))
+    full.render()
+    part = _smoke_renderer(6, str(tmp_path / 'part.png'))
+    part.clear_accumulation_buffer()
+    for i in range(4):
+        part.render_sample(i)
+    part.current_sample = 4
+    ck = str(tmp_path / 'loop.npz')
+    part.save_checkpoint(ck)
+    res = _smoke_renderer(6, str(tmp_path / 'resumed.png'))
+    res.load_checkpoint(ck)
+    res.render(resume=True)
+    assert np.array_equal(res.accum.cpu().numpy(), full.accum.cpu().numpy())
+
+
 def test_checkpoint_refuses_another_render(tmp_path):
     part = _smoke_renderer(2, str(tmp_path / 'part.png'))
     part.render()
@@ -201,5 +220,9 @@ def test_rr_statistics_match_the_oracle(tmp_path):
     _, ost = oracle_render('wavefront_comparison', 400, 'mk', (0, 0, 400, 225), 0, 4)
     assert st['killed'] == ost['rr'] > 0 and st['depth_cap'] == ost['depth_cap']
     assert st['paths'] == ost['paths'] == 400 * 225 * 4
+    # the reference's keys (renderer.py:493-500); what the device does not count is None
+    assert {'killed', 'survived', 'total_rr_paths', 'kill_rate', 'avg_depth_killed',
+            'avg_depth_survived'} <= set(st)
+    assert st['survived'] is None and st['kill_rate'] == 100.0 * st['killed'] / st['paths']
     r.setup_live_preview(250)  # GUI hooks: headless no-ops
     assert r.update_preview_if_needed() is None

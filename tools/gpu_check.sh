@@ -1,11 +1,37 @@
-# full GPU suite + 2-rank gloo rehearsal of the multi-GPU bench + C2 bench
-set -o pipefail
-O=gpurun_out/check; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAIL; grep -E "FAILED|Error|^E " $O/tests.log | head -20; exit 1; }
-grep -E "passed|failed" $O/tests.log | tail -1
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 8 > $O/dist2.json 2> $O/dist2.err || { echo DIST_FAIL; tail -20 $O/dist2.err; exit 1; }
-tail -1 $O/dist2.json | cut -c 1-600
-timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { echo BENCH_FAIL; tail $O/bench_c2.err; exit 1; }
-tail -1 $O/bench_c2.json | cut -c 1-300
-timeout -k 10 300 python bench.py --preset c4 > $O/bench_c4.json 2> $O/bench_c4.err || { echo BENCH_FAIL; tail $O/bench_c4.err; exit 1; }
-tail -1 $O/bench_c4.json | cut -c 1-300
+#!/bin/bash
+# GPU check at HEAD (not product). Usage: bash tools/gpu_check.sh OUT [STEP ...]
+# Steps (default: tests smoke c2 c3):
+#   tests        full `pytest -m gpu` suite
+#   smoke        __graft_entry__.smoke()
+#   c2|c3|c4|c5  bench.py --preset <c> (one JSON line)
+#   trace_<c>    rocprofv3 --kernel-trace --stats of the bench command
+#   fetch_<c> / write_<c>   FETCH_SIZE / WRITE_SIZE PMC passes (4 steps)
+#   dist2        2-rank gloo rehearsal of the multi-GPU bench on the one GPU
+# Every step has its own time limit; the script stops at the first failure.
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$1; shift
+mkdir -p "$OUT"
+STEPS=${*:-tests smoke c2 c3}
+step() {
+  local n=$1 t=$2; shift 2
+  echo "=== $n $(date +%T)"
+  timeout -k 10 "$t" "$@" > "$OUT/$n.log" 2>&1
+  local rc=$?
+  tail -n 1 "$OUT/$n.log" | cut -c 1-400
+  echo "=== $n rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+for s in $STEPS; do
+  case $s in
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    c2|c3|c4|c5) step bench_$s 300 python bench.py --preset $s ;;
+    trace_*) c=${s#trace_}; step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o $c -- python bench.py --preset $c --no-cpu-baseline ;;
+    fetch_*) c=${s#fetch_}; step $s 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch_$c -- python bench.py --preset $c --steps 4 --no-cpu-baseline ;;
+    write_*) c=${s#write_}; step $s 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o write_$c -- python bench.py --preset $c --steps 4 --no-cpu-baseline ;;
+    dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 8 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
