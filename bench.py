@@ -18,9 +18,9 @@ per GPU. By default the image is tile-sharded (BASELINE.json
 configs[4]): rank r renders the interleaved row bands it owns for every sample
 of every step, so the total workload (W x H x spp_per_step x steps) is fixed
 and N GPUs split it (strong scaling); the bands' height is chosen so every
-rank owns the same number of rows. One RCCL reduce (sum) of the f32
-accumulators onto rank 0, inside the timed region, assembles the image, which
-is bit-identical to the 1-GPU render. value = total samples / max-over-ranks
+rank owns the same number of rows. One RCCL gather of each rank's owned rows
+onto rank 0, inside the timed region, assembles the image
+(ptmi.distributed.assemble_image), which is bit-identical to the 1-GPU render. value = total samples / max-over-ranks
 wall time. --shard samples keeps the weak-scaling alternative (every rank the
 whole image, disjoint sample indices).
 
@@ -98,7 +98,7 @@ def parse(argv=None):
     p.add_argument('--save-image', default='')
     p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
                    help='nccl = RCCL over xGMI (the product path); gloo only to rehearse the multi-rank flow '
-                        'with several ranks on one GPU (host-side reduce)')
+                        'with several ranks on one GPU (host-side collective)')
     p.add_argument('--no-overlap', action='store_true',
                    help='megakernel: each step waits for the previous one to finish (default: consecutive '
                         'steps overlap, Integrator.render_mk_overlapped)')
@@ -248,10 +248,17 @@ def describe(a, W, H, world, shard):
         'band_rows': shard.band()[0] if a.shard == 'tiles' and world > 1 else None,
         'rows_per_rank': rows_rank,
         'max_depth': a.max_depth, 'seed': a.seed,
-        'parallelism': (f'{a.shard}-shard x{world} + {"RCCL" if a.dist_backend == "nccl" else "gloo"} reduce'
+        'parallelism': (f'{a.shard}-shard x{world} + {"RCCL" if a.dist_backend == "nccl" else "gloo"} '
+                        f'{"gather of owned row bands" if a.shard == "tiles" else "sum-reduce"}'
                         if world > 1 else 'single GPU'),
     }
     return total_spp, ('weak' if a.shard == 'samples' else 'strong'), cfg
+
+
+def throughput(samples_all, elapsed_max_s):
+    """`value` of the JSON line: every rank's samples / the slowest rank's
+    wall time (max over ranks, barrier-bracketed), in Msamples/s."""
+    return samples_all / elapsed_max_s / 1e6
 
 
 def gather_ranks(vals, dev, world):
@@ -271,7 +278,7 @@ def main():
     import torch
     import torch.distributed as dist
     from ptmi import _lib
-    from ptmi.distributed import max_over_ranks, reduce_accum
+    from ptmi.distributed import assemble_image, max_over_ranks
 
     world = a.gpus
     rank = int(os.environ.get('RANK', '0'))
@@ -301,9 +308,9 @@ def main():
         run.step(acc, k)
     # warm the collective too: RCCL sets up a collective's channels on its
     # first call, which must not land in the timed region
-    reduce_accum(acc, dst=0)
+    assemble_image(acc, shard, dst=0)
     torch.cuda.synchronize(dev)
-    acc.zero_()  # all rows: the warm-up reduce left other ranks' bands on the root
+    acc.zero_()  # all rows: the warm-up gather left other ranks' bands on the root
     integ.reset_counters()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -325,9 +332,9 @@ def main():
             run.step(acc, a.warmup + k)
         t_render_end = None
         if world > 1:
-            torch.cuda.synchronize(dev)  # this rank's own render time (per-rank balance), then the reduce
+            torch.cuda.synchronize(dev)  # this rank's own render time (per-rank balance), then the gather
             t_render_end = time.perf_counter()
-        reduce_accum(acc, dst=0)
+        assemble_image(acc, shard, dst=0)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -345,7 +352,7 @@ def main():
     rows_rank = run.rows
     samples_rank = W * rows_rank * sps * a.steps
     samples_all = samples_rank * world if a.shard == 'samples' else W * H * sps * a.steps
-    value = samples_all / elapsed / 1e6
+    value = throughput(samples_all, elapsed)
     total_spp, scaling, config = describe(a, W, H, world, shard)
 
     prof = kt.result

@@ -14,8 +14,15 @@ exchange during rendering. Two partitions:
   sample indices (weak scaling: fixed work per GPU); the sum-reduce adds the
   partial accumulators (equal to the 1-GPU render up to f32 summation order).
 
-The collective is a single ``reduce`` (RCCL over xGMI on MI355X; gloo in the
-CPU tests): W*H*3*4 bytes = 7.7 MB at 800x800, once per render.
+Image assembly is one collective per render (RCCL over xGMI on MI355X; gloo
+in the CPU tests), ``assemble_image``:
+* tiles: a ``gather`` of each rank's owned row bands onto the root (no
+  arithmetic, so the image is bit-identical to one GPU; each non-root rank
+  sends only its own rows, W*rows*12 bytes: 7.7 MB / 8 at 800x800, 99.5 MB / 8
+  at 3840x2160, instead of reducing a full-frame accumulator that is 7/8
+  zeros);
+* samples: a sum-``reduce`` of the full accumulators (every rank holds every
+  pixel).
 """
 from __future__ import annotations
 
@@ -86,3 +93,38 @@ def max_over_ranks(value, device=None, group=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def assemble_image(accum, shard, dst=0, group=None):
+    """Assemble the image of a sharded render on `dst` (in place).
+
+    tiles: every rank owns whole rows (shard.rows), so the root needs only the
+    other ranks' rows, copied, not added: each rank packs its rows into a
+    (max_rows, W, 3) buffer (max_rows = the largest rank share, so every
+    gather buffer has one shape) and one ``gather`` brings them to the root,
+    which writes them into its accumulator. samples: ``reduce_accum``.
+    No-op for world 1."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) <= 1:
+        return accum
+    if shard.mode != 'tiles':
+        return reduce_accum(accum, dst, group)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    H = accum.shape[0]
+    rows_of = [Shard(r, world, 'tiles', shard.band_rows).rows(H) for r in range(world)]
+    max_rows = max(len(r) for r in rows_of)
+    host = accum.is_cuda and dist.get_backend(group) == 'gloo'  # rehearsal backend: host buffers
+    dev = torch.device('cpu') if host else accum.device
+    mine = torch.tensor(rows_of[rank], dtype=torch.long, device=accum.device)
+    send = torch.zeros((max_rows,) + tuple(accum.shape[1:]), dtype=accum.dtype, device=accum.device)
+    send[:len(rows_of[rank])] = accum.index_select(0, mine)
+    send = send.to(dev)
+    recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, gather_list=recv, dst=dst, group=group)
+    if rank == dst:
+        for r in range(world):
+            if r != rank and rows_of[r]:
+                idx = torch.tensor(rows_of[r], dtype=torch.long, device=accum.device)
+                accum.index_copy_(0, idx, recv[r][:len(rows_of[r])].to(accum.device))
+    return accum

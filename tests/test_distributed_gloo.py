@@ -5,6 +5,8 @@ kernels themselves are covered by the -m gpu parity tests) and the product's
 ptmi.distributed.reduce_accum assembles the image on rank 0:
   * tiles   -> bit-identical to the single-device render,
   * samples -> equal up to f32 summation order.
+bench.py's own bookkeeping (balanced bands, the band gather it times,
+gather_ranks, value) is run at world sizes 2, 4 and 8.
 """
 import os
 import socket
@@ -80,7 +82,7 @@ def _bench_worker(rank, world, port, out_path):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     import bench
     from parity_helpers import oracle_render
-    from ptmi.distributed import Shard, reduce_accum
+    from ptmi.distributed import Shard, assemble_image
     a = bench.parse(['--preset', 'c2', '--gpus', str(world), '--width', str(WIDTH), '--spp-per-step', str(SPS),
                      '--steps', str(STEPS), '--dist-backend', 'gloo'])
     H = WIDTH
@@ -94,7 +96,7 @@ def _bench_worker(rank, world, port, out_path):
     ranks = bench.gather_ranks([rank, len(rows)], 'cpu', world)
     total_spp, scaling, cfg = bench.describe(a, WIDTH, H, world, sh)
     t = torch.from_numpy(acc)
-    reduce_accum(t, dst=0)
+    assemble_image(t, sh, dst=0)  # the collective bench.py times
     if rank == 0:
         np.save(out_path, t.numpy())
         with open(out_path + '.json', 'w') as f:
@@ -120,3 +122,68 @@ def test_bench_tile_partition_two_ranks(tmp_path):
 def oracle_render_full():
     from parity_helpers import oracle_render
     return oracle_render(SCENE, WIDTH, 'mk', (0, 0, WIDTH, WIDTH), 0, SPS * STEPS)
+
+
+def _bookkeeping_worker(rank, world, port, height, width, out_path):
+    """bench.py's tiles bookkeeping at the BASELINE heights on gloo: balanced
+    bands (Shard.balanced), each rank's owned rows filled with the one-rank
+    image (a seeded stand-in: the kernels are covered by the -m gpu tests and
+    rendering 800 or 2160 rows with the oracle would take minutes), the image
+    assembled by ptmi.distributed.assemble_image (the gather bench.py times),
+    per-rank rows gathered (gather_ranks), value = all samples / max wall."""
+    import json
+    import sys
+    for p in (ROOT, os.path.join(ROOT, 'path-tracer-python_amd'), os.path.join(ROOT, 'tests')):
+        sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import bench
+    from ptmi.distributed import Shard, assemble_image, max_over_ranks
+    a = bench.parse(['--preset', 'c2', '--gpus', str(world), '--dist-backend', 'gloo'])
+    sh = Shard.balanced(rank, world, a.shard, height)
+    img = np.random.default_rng(7).standard_normal((height, width, 3)).astype(np.float32)
+    acc = np.zeros_like(img)
+    rows = sh.rows(height)
+    acc[rows] = img[rows]
+    t = torch.from_numpy(acc)
+    assemble_image(t, sh, dst=0)
+    elapsed_rank = 1.0 + 0.125 * rank  # per-rank wall times; the slowest sets value
+    samples_rank = width * len(rows) * a.spp_per_step * a.steps
+    ranks = bench.gather_ranks([rank, len(rows), samples_rank, elapsed_rank], 'cpu', world)
+    elapsed = max_over_ranks(elapsed_rank)
+    value = bench.throughput(width * height * a.spp_per_step * a.steps, elapsed)
+    _, scaling, cfg = bench.describe(a, width, height, world, sh)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+        with open(out_path + '.json', 'w') as f:
+            json.dump({'ranks': ranks, 'value': value, 'elapsed': elapsed, 'band': sh.band_rows,
+                       'scaling': scaling, 'parallelism': cfg['parallelism'], 'spp': a.spp_per_step * a.steps}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world, height', [(4, 800), (8, 800), (4, 2160), (8, 2160)])
+def test_bench_tiles_bookkeeping_at_scale(tmp_path, world, height):
+    """World sizes 4 and 8 at 800 and 2160 rows: every row assembled on rank 0
+    exactly once and bit-identical to the one-rank image, balanced rows,
+    value = samples / max-over-ranks wall time."""
+    import json
+    width = 8
+    out = str(tmp_path / f'bk_{world}_{height}.npy')
+    mp.start_processes(_bookkeeping_worker, args=(world, _free_port(), height, width, out), nprocs=world,
+                       start_method='spawn')
+    img = np.random.default_rng(7).standard_normal((height, width, 3)).astype(np.float32)
+    assert np.array_equal(np.load(out), img)  # every row copied from its owner, no arithmetic
+    with open(out + '.json') as f:
+        rec = json.load(f)
+    rows = [int(r[1]) for r in rec['ranks']]
+    assert [int(r[0]) for r in rec['ranks']] == list(range(world)) and sum(rows) == height
+    assert max(rows) - min(rows) <= rec['band']  # balanced to within one band
+    if (world, height) == (8, 800):
+        assert rec['band'] == 4 and rows == [100] * 8
+    if (world, height) == (8, 2160):
+        assert rec['band'] == 8 and max(rows) == 272
+    want_elapsed = 1.0 + 0.125 * (world - 1)
+    assert rec['elapsed'] == want_elapsed
+    assert rec['value'] == width * height * rec['spp'] / want_elapsed / 1e6
+    assert rec['scaling'] == 'strong' and 'gather of owned row bands' in rec['parallelism']

@@ -143,6 +143,7 @@ def test_checkpoint_after_render_sample_loop_resumes(tmp_path):
     full = _smoke_renderer(6, str(tmp_path / 'full.png'))
     full.render()
     part = _smoke_renderer(6, str(tmp_path / 'part.png'))
+    part._upload_camera_to_gpu()  # picks up background_color, as InteractiveViewer does before its loop
     part.clear_accumulation_buffer()
     for i in range(4):
         part.render_sample(i)

@@ -7,6 +7,11 @@
 #   trace_<c>    rocprofv3 --kernel-trace --stats of the bench command
 #   fetch_<c> / write_<c>   FETCH_SIZE / WRITE_SIZE PMC passes (4 steps)
 #   dist2        2-rank gloo rehearsal of the multi-GPU bench on the one GPU
+#   ab_wf_c3 / ab_wf_fog / ab_mk_c2 / ab_mk_c4 / ab_mk_c5
+#                A/B timing (tools/gpu_ab.sh) of every variants/*.so against
+#                the default build: wavefront on vol2 800x800 or the mesh-fog
+#                scene, megakernel on C2 / C4 / C5 shapes
+#   parity_variants  the GPU parity tests against each variants/*.so
 # Every step has its own time limit; the script stops at the first failure.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -31,6 +36,13 @@ for s in $STEPS; do
     fetch_*) c=${s#fetch_}; step $s 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch_$c -- python bench.py --preset $c --steps 4 --no-cpu-baseline ;;
     write_*) c=${s#write_}; step $s 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o write_$c -- python bench.py --preset $c --steps 4 --no-cpu-baseline ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 8 ;;
+    ab_wf_c3) step $s 900 env AB_MODES=wf bash tools/gpu_ab.sh ;;
+    ab_wf_fog) step $s 900 env AB_MODES=wf AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
+    ab_mk_c2) step $s 900 env AB_MODES=mk bash tools/gpu_ab.sh ;;
+    ab_mk_c4) step $s 900 env AB_MODES=mk AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
+    ab_mk_c5) step $s 900 env AB_MODES=mk AB_SCENE=vol2_final_scene_comparison AB_WIDTH=3840 AB_SPP=16 bash tools/gpu_ab.sh ;;
+    parity_variants) for lib in path-tracer-python_amd/ptmi/_lib/variants/*.so; do
+        step parity_$(basename $lib .so) 600 env PTMI_LIB=$PWD/$lib python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edge.py -x -q --timeout 300 --timeout-method thread; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
