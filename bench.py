@@ -141,29 +141,55 @@ def load_workload(scene, width):
             'no external dataset')
 
 
+def cpu_info():
+    """CPU model and core counts of this host: the model from /proc/cpuinfo,
+    os.cpu_count() (every CPU of the machine) and the CPUs this process may
+    run on (sched_getaffinity)."""
+    model = None
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 1
+    return {'cpu_model': model, 'os_cpu_count': os.cpu_count(), 'affinity_cpus': allowed}
+
+
 def cpu_baseline(sa, cam, bg, scene, variant, max_depth, seed, budget_s):
-    """Time the CPU oracle on a bounded slice of the workload (rank 0, N=1)."""
+    """Time the CPU oracle on a bounded sample of the workload (rank 0, N=1):
+    the whole frame (every pixel, so the sample has the workload's mix of sky,
+    fog and geometry) at as many samples per pixel as fit the time budget,
+    after a 1-spp whole-frame calibration pass. Threads: OMP_NUM_THREADS when
+    set (the GPU box sets it to the CPU share of one GPU, 16), else every CPU
+    this process may run on."""
     import numpy as np
     import oracle
     W, H = cam['width'], cam['height']
-    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+    info = cpu_info()
+    env = os.environ.get('OMP_NUM_THREADS')
+    threads = int(env) if env and env.isdigit() and int(env) > 0 else info['affinity_cpus']
     osc = oracle.OracleScene(sa)
     fr = oracle.make_frame(cam, bg, max_depth, seed, W, H)
     acc = np.zeros((H, W, 3), np.float32)
-    rows = min(H, 64)
-    y0 = (H - rows) // 2
     t = time.perf_counter()
-    oracle.render(osc, fr, variant, acc, (0, y0, W, rows), 0, 1, threads)
+    oracle.render(osc, fr, variant, acc, (0, 0, W, H), 0, 1, threads)
     t1 = time.perf_counter() - t
     spp = max(1, int(budget_s / max(t1, 1e-3)))
     t = time.perf_counter()
-    oracle.render(osc, fr, variant, acc, (0, y0, W, rows), 1, spp, threads)
+    oracle.render(osc, fr, variant, acc, (0, 0, W, H), 1, spp, threads)
     dt = time.perf_counter() - t
-    n = W * rows * spp
+    n = W * H * spp
     return {'value': round(n / dt / 1e6, 4), 'unit': 'Msamples/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{scene} {W}x{H}, rows {y0}..{y0 + rows - 1} ({W}x{rows} px) x {spp} spp, '
-                      f'{"wavefront" if variant == "wf" else "megakernel"} semantics, C oracle '
-                      f'(restatement of kernels.py; Taichi ti.cpu absent), {dt:.1f} s'}
+            'threads_source': 'OMP_NUM_THREADS' if env else 'sched_getaffinity', **info,
+            'sample': f'{scene} {W}x{H}, the whole frame x {spp} spp (samples 1..{spp}, after a 1-spp '
+                      f'calibration pass), {"wavefront" if variant == "wf" else "megakernel"} semantics, C oracle '
+                      f'(restatement of kernels.py; Taichi ti.cpu absent), {threads} OpenMP threads, {dt:.1f} s'}
 
 
 TRAFFIC_FILE = os.path.join(ROOT, 'profiles', 'traffic.json')

@@ -83,3 +83,13 @@ def test_balanced_bands_cover_every_row_once(H, world):
     assert (seen == 1).all()
     best = -(-H // world)
     assert max(sizes) <= max(best * 1.01, best + 1) or H < world * 8
+
+
+def test_cpu_baseline_records_the_host_and_times_the_whole_frame():
+    """cpu_baseline (bench.py's CPU leg): the whole frame of the workload, the
+    CPU model, os.cpu_count(), the allowed CPUs and the threads used."""
+    sa, cam, bg, _ = bench.load_workload('wavefront_comparison', 400)
+    r = bench.cpu_baseline(sa, cam, bg, 'wavefront_comparison', 'mk', 50, 0, 0.2)
+    assert r['kind'] == 'port' and r['value'] > 0 and r['unit'] == 'Msamples/s'
+    assert r['os_cpu_count'] >= r['affinity_cpus'] >= 1 and r['cores'] >= 1
+    assert 'cpu_model' in r and 'the whole frame' in r['sample'] and '400x225' in r['sample']

@@ -12,6 +12,9 @@
 #                the default build: wavefront on vol2 800x800 or the mesh-fog
 #                scene, megakernel on C2 / C4 / C5 shapes
 #   parity_variants  the GPU parity tests against each variants/*.so
+#   cache_mk / cache_wf   L1/L2 hit-rate PMC pass of one 32-spp call (tools/pmc_cache_summary.py reads it)
+#   lat_mk / lat_wf       VALU / wait PMC passes (tools/gpu_pmc_latency.sh; tools/pmc_valu.py reads them)
+#   probe                 the diagnostic probe builds (tools/gpu_probe.sh; variants libptmi_probe{1,2}.so)
 # Every step has its own time limit; the script stops at the first failure.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -43,6 +46,9 @@ for s in $STEPS; do
     ab_mk_c5) step $s 900 env AB_MODES=mk AB_SCENE=vol2_final_scene_comparison AB_WIDTH=3840 AB_SPP=16 bash tools/gpu_ab.sh ;;
     parity_variants) for lib in path-tracer-python_amd/ptmi/_lib/variants/*.so; do
         step parity_$(basename $lib .so) 600 env PTMI_LIB=$PWD/$lib python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edge.py -x -q --timeout 300 --timeout-method thread; done ;;
+    cache_mk|cache_wf) v=${s#cache_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_cache" -o $v -- python tools/ab.py $v 32 1 ;;
+    lat_mk|lat_wf) v=${s#lat_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_$v bash tools/gpu_pmc_latency.sh ;;
+    probe) step probe 600 bash tools/gpu_probe.sh ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
