@@ -71,8 +71,11 @@ ALGO_BYTES = {
     # S = measured segments/sample: the bytes the reference's stage pipeline
     # must move for one camera path (the megakernel keeps them in registers)
     'megakernel': ('samples', None),
-    # camera ray record write, 48 B per ray
-    'wf_generate': ('rays', 48),
+    # initial slot state (item word) per slot
+    'wf_generate': ('rays', 4),
+    # a batch's tail, every remaining path in one launch: per segment the
+    # intersect and scatter figures together (32 + 108 B)
+    'wf_drain': ('rays', 140),
     # accumulator read + write 24 B + batch x 12 B staging read, per pixel
     'wf_resolve': ('pixels', 24),
     # accumulator read + write 24 B + batch x 12 B staging read, per pixel
@@ -394,7 +397,7 @@ def main():
         unit_bytes = b_sample
     units = {'wf_intersect': cnt['segments'], 'wf_scatter': cnt['segments'],
              'megakernel': samples_rank,
-             'wf_generate': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
+             'wf_generate': 0, 'wf_drain': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
              'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]
     dom_ms = prof[dom]['busy_ms']
     launches = prof[dom]['launches']

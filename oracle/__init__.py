@@ -60,18 +60,24 @@ def load():
     if _lib is None:
         if not os.path.exists(LIB):
             build()
-        lib = C.CDLL(LIB)
-        lib.or_render.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, P, C.c_int, C.c_int, C.c_int,
-                                  C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OrStats)]
-        lib.or_traverse.argtypes = [C.POINTER(OrScene), C.c_int, P, P, C.c_float, C.c_float, P, P, P]
-        lib.or_trace_path.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, C.c_int, C.c_int, C.c_int,
-                                      P, C.POINTER(OrStats)]
-        lib.or_math_probe.argtypes = [C.c_int, P, P, P, C.c_int]
-        lib.or_rng_probe.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, P, P]
-        lib.or_func_probe.argtypes = [C.POINTER(OrScene), C.c_int, P, P, C.c_int]
-        lib.or_func_probe.restype = C.c_int
-        _lib = lib
+        _lib = load_variant(LIB)
     return _lib
+
+
+def load_variant(path):
+    """A libptoracle build at `path` (the tests' negative-control builds of
+    pt_oracle.c with a switch changed), with the entry points typed."""
+    lib = C.CDLL(path)
+    lib.or_render.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, P, C.c_int, C.c_int, C.c_int,
+                              C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OrStats)]
+    lib.or_traverse.argtypes = [C.POINTER(OrScene), C.c_int, P, P, C.c_float, C.c_float, P, P, P]
+    lib.or_trace_path.argtypes = [C.POINTER(OrScene), C.POINTER(OrFrame), C.c_int, C.c_int, C.c_int, C.c_int,
+                                  P, C.POINTER(OrStats)]
+    lib.or_math_probe.argtypes = [C.c_int, P, P, P, C.c_int]
+    lib.or_rng_probe.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, P, P]
+    lib.or_func_probe.argtypes = [C.POINTER(OrScene), C.c_int, P, P, C.c_int]
+    lib.or_func_probe.restype = C.c_int
+    return lib
 
 
 def _ptr(a):
@@ -150,13 +156,14 @@ def make_frame(cam, bg, max_depth, seed, width, height, traversal='stack'):
     return f
 
 
-def render(oscene, frame, variant, accum, window, s_begin, s_count, threads=0):
-    """variant: 'mk' | 'wf'. accum (H, W, 3) f32 numpy, updated in place."""
+def render(oscene, frame, variant, accum, window, s_begin, s_count, threads=0, lib=None):
+    """variant: 'mk' | 'wf'. accum (H, W, 3) f32 numpy, updated in place.
+    lib: a load_variant() build instead of the oracle."""
     assert accum.dtype == np.float32 and accum.flags['C_CONTIGUOUS']
     assert accum.shape == (frame.height, frame.width, 3)
     x0, y0, w, h = window
     st = OrStats()
-    rc = load().or_render(C.byref(oscene.s), C.byref(frame), 0 if variant == 'mk' else 1, _ptr(accum),
+    rc = (lib or load()).or_render(C.byref(oscene.s), C.byref(frame), 0 if variant == 'mk' else 1, _ptr(accum),
                           x0, y0, w, h, s_begin, s_count, threads, C.byref(st))
     if rc != 0:
         raise RuntimeError(f'or_render failed: {rc}')

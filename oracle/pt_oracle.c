@@ -248,7 +248,10 @@ static int traverse_bvh(const or_scene *sc, pt_v3 o, pt_v3 d, float tmin, float 
     pt_v3 inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f,
                        fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
                        fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);
-    int32_t stack[64];
+#ifndef OR_STACK_SLOTS
+#define OR_STACK_SLOTS 64   /* kernels.py:649; other values only for the tests' overflow control */
+#endif
+    int32_t stack[OR_STACK_SLOTS];
     int sp = 0;
     stack[sp++] = 0;
     int any = 0;
@@ -281,15 +284,15 @@ static int traverse_bvh(const or_scene *sc, pt_v3 o, pt_v3 d, float tmin, float 
                 float ld = pt_dot(pt_sub(lc, o), d);
                 float rd = pt_dot(pt_sub(rc, o), d);
                 if (ld < rd) {
-                    if (sp < 64) stack[sp++] = r;
-                    if (sp < 64) stack[sp++] = l;
+                    if (sp < OR_STACK_SLOTS) stack[sp++] = r;
+                    if (sp < OR_STACK_SLOTS) stack[sp++] = l;
                 } else {
-                    if (sp < 64) stack[sp++] = l;
-                    if (sp < 64) stack[sp++] = r;
+                    if (sp < OR_STACK_SLOTS) stack[sp++] = l;
+                    if (sp < OR_STACK_SLOTS) stack[sp++] = r;
                 }
             } else {
-                if (r >= 0 && sp < 64) stack[sp++] = r;
-                if (l >= 0 && sp < 64) stack[sp++] = l;
+                if (r >= 0 && sp < OR_STACK_SLOTS) stack[sp++] = r;
+                if (l >= 0 && sp < OR_STACK_SLOTS) stack[sp++] = l;
             }
         }
     }

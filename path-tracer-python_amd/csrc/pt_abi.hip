@@ -87,9 +87,12 @@ static int to_dev_scene(const ptmi_scene_view* s, DevScene& d) {
   if (s->num_images < 0 || s->num_images > PTMI_MAX_IMAGES) return fail(PTMI_EINVAL, "num_images");
   if (s->num_images > 0 && !s->texels) return fail(PTMI_EINVAL, "texels");
   // The reference's 64-slot stack never overflows for leaf depth <= 62
-  // (kernels.py:719-740); beyond that its silent drops are not reproduced.
-  if (s->max_leaf_depth < 0 || s->max_leaf_depth > 62)
-    return fail(PTMI_ECAPACITY, "BVH leaf depth %d exceeds 62", s->max_leaf_depth);
+  // (kernels.py:719-740); deeper BVHs run its exact walk on its own nodes,
+  // silent drops included (TravRS, pt_device.hpp), which needs ref_nodes.
+  if (s->max_leaf_depth < 0) return fail(PTMI_EINVAL, "negative max_leaf_depth");
+  if (s->max_leaf_depth > 62 && np > 0 && !s->ref_nodes)
+    return fail(PTMI_EINVAL, "BVH leaf depth %d > 62 needs ref_nodes (the reference's 64-entry stack walk)",
+                s->max_leaf_depth);
   if (s->num_bvh_nodes != (np > 0 ? 2 * np - 1 : 0))
     return fail(PTMI_EINVAL, "num_bvh_nodes %d for %d primitives (expected 2N-1)", s->num_bvh_nodes, np);
   if (s->ref_nodes && !aligned16(s->ref_nodes)) return fail(PTMI_EINVAL, "ref_nodes misaligned");

@@ -662,7 +662,105 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4*, Tra
   }
 }
 
-// Traversal state type by frame.traversal (PTMI_TRAV_*).
+// ---------------------------------------------------------------- reference stack (deep BVHs)
+// traverse_bvh_legacy (kernels.py:625-742) exactly as the reference runs it,
+// for BVHs whose leaf depth exceeds 62: a 64-entry stack of node indices; the
+// box of a popped node is tested against [t_min, closest_t] (:667); an
+// internal node pushes both children unconditionally, the far one first by
+// projected child-centre distance (:705-732; a missing child is skipped,
+// :733-740), and a push is dropped once the stack holds 64 entries (the
+// `if stack_ptr < 64` guards, :719-740). Trav (children culled at push, one
+// slot per hit child) gives the same hits while no push is dropped, which
+// leaf depth <= 62 guarantees; past that, the reference's dropped pushes are
+// part of its result, so the dispatch runs this walk (kTravRefStack, STACK
+// 64) on the reference's own nodes (ref_nodes) instead. Slot .x = node index.
+constexpr int kTravRefStack = 2;  // internal: chosen by the dispatch (leaf depth > 62), not a frame setting
+constexpr int kRefStackSlots = 64;  // kernels.py:649
+struct TravRS {
+  pt_v3 inv;
+  float tmin, closest;
+  int32_t best;  // leaf code of the closest hit; 0 = none
+  uint32_t sp, sp0;
+#if PTMI_PROBE == 2
+  uint32_t probe;
+#endif
+  __device__ __forceinline__ bool any() const { return best != 0; }
+  __device__ __forceinline__ bool busy() const { return sp != sp0; }
+  __device__ __forceinline__ void init(Stack st) { sp = sp0 = lds_addr(st.slot0); }
+};
+
+template <int STACK, int SB = kBlock>
+__device__ __forceinline__ void trav_begin(const DevScene& sc, TravRS& tr, Stack st, pt_v3 d, pt_v3 o, float tmin,
+                                           float tmax) {
+  static_assert(STACK >= kRefStackSlots, "the reference stack has 64 entries");
+  (void)o;
+  tr.inv = pt_v3f(fabsf(d.x) > 1e-8f ? 1.0f / d.x : 1e8f, fabsf(d.y) > 1e-8f ? 1.0f / d.y : 1e8f,
+                  fabsf(d.z) > 1e-8f ? 1.0f / d.z : 1e8f);  // kernels.py:642-646 (Q15)
+  tr.tmin = tmin;
+  tr.closest = tmax;
+  tr.best = 0;
+  tr.init(st);
+  if (sc.n_nodes > 0) {  // the root (:649-652); with no nodes the reference pops and skips it
+    lds_store2(tr.sp, 0u, 0u);
+    tr.sp += SB * 8;
+  }
+}
+
+// One iteration of the reference's while loop (kernels.py:654-740).
+template <int STACK, int SB = kBlock, int DEFER = 0, int LDS = STACK>
+__device__ __forceinline__ void trav_step(const DevScene& sc, const float4*, TravRS& tr, Stack, pt_v3 o, pt_v3 d) {
+  constexpr uint32_t kSlot = SB * 8;
+  tr.sp -= kSlot;
+  const int32_t ni = (int32_t)lds_load2(tr.sp).x;
+  if (ni < 0 || ni >= sc.n_nodes) return;  // :660-661
+  const float4* nd = sc.ref_nodes + 3 * ni;
+  const float4 s0 = nd[0], s1 = nd[1], s2 = nd[2];
+  const float t0x = (s0.x - o.x) * tr.inv.x, t1x = (s1.x - o.x) * tr.inv.x;  // hit_aabb_optimized :601-621
+  const float t0y = (s0.y - o.y) * tr.inv.y, t1y = (s1.y - o.y) * tr.inv.y;
+  const float t0z = (s0.z - o.z) * tr.inv.z, t1z = (s1.z - o.z) * tr.inv.z;
+  const float lo = pt_maxf(pt_maxf(pt_minf(t0x, t1x), pt_minf(t0y, t1y)), pt_maxf(pt_minf(t0z, t1z), tr.tmin));
+  const float hi = pt_minf(pt_minf(pt_maxf(t0x, t1x), pt_maxf(t0y, t1y)), pt_minf(pt_maxf(t0z, t1z), tr.closest));
+  if (!(hi >= lo)) return;  // :667-668
+  const int32_t code = __float_as_int(s2.y);
+  if (code != 0) {  // leaf :671-697
+#if PTMI_PROBE == 2
+    tr.probe |= leaf_type(code) == kSphere ? 1 : 2;
+#endif
+    float t;
+    if (hit_leaf(sc, code, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
+      tr.closest = t;
+      tr.best = code;
+    }
+    return;
+  }
+#if PTMI_PROBE == 2
+  tr.probe |= 4;
+#endif
+  const int32_t left = __float_as_int(s0.w), right = __float_as_int(s1.w);
+  const uint32_t cap = tr.sp0 + (uint32_t)kRefStackSlots * kSlot;  // `stack_ptr < 64`
+  int32_t first = right, second = left;  // one child only: right, then left (:733-740)
+  if (left >= 0 && right >= 0) {         // far child first (:705-732)
+    const float4* ln = sc.ref_nodes + 3 * left;
+    const float4* rn = sc.ref_nodes + 3 * right;
+    const float4 l0 = ln[0], l1 = ln[1], r0 = rn[0], r1 = rn[1];
+    const pt_v3 lc = pt_v3f((l0.x + l1.x) * 0.5f, (l0.y + l1.y) * 0.5f, (l0.z + l1.z) * 0.5f);
+    const pt_v3 rc = pt_v3f((r0.x + r1.x) * 0.5f, (r0.y + r1.y) * 0.5f, (r0.z + r1.z) * 0.5f);
+    if (!(pt_dot(pt_sub(lc, o), d) < pt_dot(pt_sub(rc, o), d))) {
+      first = left;
+      second = right;
+    }
+  }
+  if (first >= 0 && tr.sp < cap) {
+    lds_store2(tr.sp, (uint32_t)first, 0u);
+    tr.sp += kSlot;
+  }
+  if (second >= 0 && tr.sp < cap) {
+    lds_store2(tr.sp, (uint32_t)second, 0u);
+    tr.sp += kSlot;
+  }
+}
+
+// Traversal state type by frame.traversal (PTMI_TRAV_*), or kTravRefStack.
 template <int TRAV>
 struct TravOf {
   typedef Trav T;
@@ -670,6 +768,10 @@ struct TravOf {
 template <>
 struct TravOf<PTMI_TRAV_STACKLESS> {
   typedef TravSL T;
+};
+template <>
+struct TravOf<kTravRefStack> {
+  typedef TravRS T;
 };
 
 #ifndef PTMI_TRAV_UNROLL

@@ -97,6 +97,23 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // +7.5 %, C5 +6.3 %, C4 +8 % with the shading threshold at 24 (0 = off).
 #define PTMI_MK_DEFER 12
 #endif
+#ifndef PTMI_MK_SHADE_DEFER
+// Shading-round deferral by material kind (0 = off). A shading round runs the
+// union of its lanes' material code, one branch after another for disjoint
+// lane sets (34 % of a wave's cycles on C2, profiles/r03/probe_r3.txt). With
+// deferral, a lane whose traced segment needs an expensive kind of shading
+// (medium free flight, Lambertian, Perlin, glossy, dielectric: shade_kind)
+// keeps its result and waits while fewer than PTMI_MK_SHADE_DEFER lanes of
+// the wave need the same kind, unless PTMI_MK_SHADE_DEFER_MAX lanes would be
+// left waiting or no lane is still traversing; cheap ends (a miss, a medium
+// boundary's mode switch, an emissive hit) shade at once. Each lane still
+// shades its own segments in its own order, so results are unchanged.
+#define PTMI_MK_SHADE_DEFER 0
+#endif
+#ifndef PTMI_MK_SHADE_DEFER_MAX
+#define PTMI_MK_SHADE_DEFER_MAX 16
+#endif
+
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -195,6 +212,38 @@ static int64_t mk_tiles(const DevFrame& fr, int32_t* tx_out = nullptr) {
   const int64_t tx = (fr.w + tw - 1) / tw, ty = (fr.n_rows + th - 1) / th;
   if (tx_out) *tx_out = (int32_t)tx;
   return tx * ty;
+}
+
+// Shading kind of a traced segment (PTMI_MK_SHADE_DEFER): 0 cheap (a miss, a
+// medium boundary's switch to the exit search, an emissive surface), 1 the
+// medium's free flight after its exit search, 2 Lambertian, 3 Perlin-textured,
+// 4 glossy (metal, isotropic, others), 5 dielectric. Surface kinds come from
+// the leaf code's material class (no load): classes 0..5 (PTMI_CLASS_*) map to
+// kinds 2, 4, 5, 0, 3, 0.
+constexpr int kShadeKinds = 6;
+template <class TR>
+__device__ __forceinline__ int32_t shade_kind(bool exit_mode, const TR& tr) {
+  constexpr uint32_t kKindOfClass = 2u | 4u << 3 | 5u << 6 | 0u << 9 | 3u << 12 | 0u << 15;
+  if (exit_mode) return 1;
+  if (!tr.any()) return 0;
+  return (int32_t)((kKindOfClass >> (3 * leaf_class(tr.best))) & 7u);
+}
+
+// Kinds the wave shades in this round (bit mask, wave-uniform), given which
+// lanes have a traced segment (fin) and its kind: cheap ends always; a kind
+// once PTMI_MK_SHADE_DEFER lanes have it; every kind when no lane is still
+// traversing or PTMI_MK_SHADE_DEFER_MAX lanes would be left waiting.
+__device__ __forceinline__ uint32_t shade_round_kinds(bool fin, int32_t kind, uint32_t nbusy) {
+  uint32_t run = 1u, waiting = 0u;
+#pragma unroll
+  for (int k = 1; k < kShadeKinds; ++k) {
+    const unsigned long long m = pt_ballot(fin && kind == k);
+    const uint32_t n = __builtin_popcount((uint32_t)m) + __builtin_popcount((uint32_t)(m >> 32));
+    if (n >= (uint32_t)PTMI_MK_SHADE_DEFER) run |= 1u << k;
+    else waiting += n;
+  }
+  if (nbusy == 0u || waiting >= (uint32_t)PTMI_MK_SHADE_DEFER_MAX) run = (1u << kShadeKinds) - 1u;
+  return run;
 }
 
 template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
@@ -318,13 +367,25 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #if PTMI_MK_PRIO_TRAV >= 0
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
 #endif
+#if PTMI_MK_SHADE_DEFER
+    uint32_t run_kinds = (1u << kShadeKinds) - 1u;  // kinds shaded in this round
+#endif
     for (;;) {  // traversal steps
       // a lane's stack is empty unless its segment is mid-traversal (busy => trav)
       const unsigned long long mbusy = pt_ballot(tr.busy());
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
+#if PTMI_MK_SHADE_DEFER
+      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) {
+        const bool fin = trav && !tr.busy();
+        const int32_t kind = shade_kind(ps.mode == kModeMediumExit, tr);
+        run_kinds = shade_round_kinds(fin, kind, nbusy);
+        if (pt_ballot(fin && ((run_kinds >> kind) & 1u)) != 0ull) break;
+      }
+#else
       if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
+#endif
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -352,7 +413,14 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #if PTMI_MK_PRIO_TRAV >= 0
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
-    if (trav && !tr.busy()) {  // segment traced: shade it
+#if PTMI_MK_SHADE_DEFER
+    // kinds of this round; after the loop ended with no lane traversing, all
+    if (pt_ballot(tr.busy()) == 0ull) run_kinds = (1u << kShadeKinds) - 1u;
+    const bool shade_now = trav && !tr.busy() && ((run_kinds >> shade_kind(ps.mode == kModeMediumExit, tr)) & 1u);
+#else
+    const bool shade_now = trav && !tr.busy();
+#endif
+    if (shade_now) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
       const bool hit = tr.any();
@@ -616,7 +684,9 @@ hipError_t mk_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
   if (stack_needed <= 20) return launch_mk<20>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 24) return launch_mk<24>(sc, fr, accum, s_begin, s_count, counters, stream);
   if (stack_needed <= 32) return launch_mk<32>(sc, fr, accum, s_begin, s_count, counters, stream);
-  return launch_mk<64>(sc, fr, accum, s_begin, s_count, counters, stream);
+  if (stack_needed <= kRefStackSlots - 1) return launch_mk<64>(sc, fr, accum, s_begin, s_count, counters, stream);
+  // leaf depth > 62: the reference's 64-entry stack drops pushes (TravRS)
+  return launch_mk<kRefStackSlots, kTravRefStack>(sc, fr, accum, s_begin, s_count, counters, stream);
 }
 
 // ---------------------------------------------------------------- staged
@@ -699,7 +769,9 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
   if (stack_needed <= 20) return launch_mk_trace<20>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= 24) return launch_mk_trace<24>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= 32) return launch_mk_trace<32>(sc, fr, st, s_begin, nb, counters, stream);
-  return launch_mk_trace<64>(sc, fr, st, s_begin, nb, counters, stream);
+  if (stack_needed <= kRefStackSlots - 1) return launch_mk_trace<64>(sc, fr, st, s_begin, nb, counters, stream);
+  // leaf depth > 62: the reference's 64-entry stack drops pushes (TravRS)
+  return launch_mk_trace<kRefStackSlots, kTravRefStack>(sc, fr, st, s_begin, nb, counters, stream);
 }
 
 int64_t mk_max_batch(const DevFrame& fr) {

@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 namespace ptmi {
-enum : int32_t { kProfMk = 0, kProfWfGenerate = 1, kProfWfIntersect = 2, kProfWfRetired = 3 /* wf_shade until round 3: no launches */, kProfWfScatter = 4,
+enum : int32_t { kProfMk = 0, kProfWfGenerate = 1, kProfWfIntersect = 2, kProfWfDrain = 3 /* wf_shade until round 3 */, kProfWfScatter = 4,
                  kProfWfResolve = 5, kProfMkResolve = 6, kProfKinds = 7 };
 // prof_begin returns the launch's event slot (-1: not profiling / full);
 // pass it to prof_end. Thread-safe: the session is guarded by a mutex and each

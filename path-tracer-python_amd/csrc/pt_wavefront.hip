@@ -103,24 +103,38 @@ constexpr int isect_lds() {
 #endif
 constexpr uint32_t kDead = 0xffffffffu;     // item of a retired slot
 constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (assigned in wf_intersect)
+// A slot whose camera ray was generated and traced in this iteration's
+// wf_intersect holds its item | kFresh and nothing else: the ray is not
+// stored, wf_scatter regenerates it from the item (get_ray, kernels.py:
+// 176-201: the same draws from the same counter-based stream), with
+// throughput 1 and depth 0. Items are < 2^31 (wf_render bounds them).
+constexpr uint32_t kFresh = 0x80000000u;
 
+// Ray queue: five streams per slot, each read only by the stage that needs
+// it. wf_intersect reads the item word (4 B) of every slot and the ray
+// (o, d: A + D, 24 B) of a traced one; wf_scatter reads the rest.
 struct Queue {
-  float4* a;  // o.xyz, d.x
-  float4* b;  // d.y, d.z, item (bits), rng counter (bits)
-  float4* c;  // thr.xyz, meta (bits)
+  float4* a;      // o.xyz, d.x
+  float2* d;      // d.y, d.z
+  float4* c;      // thr.xyz, meta (bits)
+  uint32_t* item; // work item (| kFresh), kPending or kDead
+  uint32_t* ctr;  // rng draw counter
 };
 
 // Closest-hit lists (wf_intersect fills them, wf_scatter drains them).
-// Each list holds kShards segments of medseg slot indices; the medium and
-// Perlin lists share one array, the Perlin one filling its segments from the top
-// (a slot is in at most one list, so together they never exceed a segment).
+// Each list holds kShards segments of medseg slot indices. Two pairs of lists
+// share one array, the second filling its segments from the top (a slot is in
+// at most one list, so together they never exceed a segment): medium and
+// Perlin; glossy and ended (misses and emissive hits: their paths end
+// without a scatter, shade_miss_rays kernels.py:1266-1280 and kernels.py:
+// 1365-1375).
 enum : int32_t { kListLambertian = 0, kListGlossy = 1, kListDielectric = 2, kListMedium = 3, kListNoise = 4,
-                 kLists = 5 };
+                 kListEnded = 5, kLists = 6 };
 
 struct WfBufs {
   Queue q;
-  float2* hit;        // t, leaf ref (bits) of a traced slot's closest hit (misses end in wf_intersect)
-  int32_t* lists;     // 4 arrays of capacity indices: Lambertian, glossy, dielectric, medium + Perlin
+  float2* hit;        // t, leaf ref (bits) of a traced slot's closest hit; ref 0 for a miss
+  int32_t* lists;     // 4 arrays of capacity indices: Lambertian, glossy + ended, dielectric, medium + Perlin
   float* staging;     // [batch][npix][3] path colours
   int32_t* ctl;       // this pipe's counters, one per 256-B line (see ctl_*)
   char* spill;        // this pipe's spilled stack slots of wf_intersect (kSpillSlots rows of its grid's threads)
@@ -165,9 +179,9 @@ __host__ __device__ __forceinline__ int32_t* ctl_list(const WfBufs& wb, int32_t 
 }
 // slot-index entry k of shard s's segment of a list
 __device__ __forceinline__ int32_t* list_slot(const WfBufs& wb, int32_t list, int32_t s, int32_t k) {
-  const int32_t arr = list < kListMedium ? list : 3;
+  const int32_t arr = list < kListMedium ? list : list == kListEnded ? kListGlossy : kListMedium;
   int32_t* seg = wb.lists + (size_t)arr * (size_t)wb.capacity + (size_t)s * (size_t)wb.medseg;
-  return list == kListNoise ? seg + wb.medseg - 1 - k : seg + k;
+  return (list == kListNoise || list == kListEnded) ? seg + wb.medseg - 1 - k : seg + k;
 }
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -220,7 +234,8 @@ __device__ __forceinline__ void block_flush(const uint32_t (&vals)[N], void* scr
 
 struct Ray {
   pt_v3 o, d, thr;
-  uint32_t item, ctr, meta;
+  uint32_t item, ctr, meta;  // item without kFresh
+  bool fresh;                // a camera ray regenerated from its item (its slot holds only the item word)
 };
 
 // Streamed buffers (queue records, hit records, medium lists, staging) go
@@ -251,33 +266,21 @@ __device__ __forceinline__ float2 h_load(const float2* p) {
 }
 __device__ __forceinline__ void h_store(float2* p, float2 v) { s_store((pt_qf2*)p, pt_qf2{v.x, v.y}); }
 
+// A continuing ray back into its slot; a fresh ray's slot also gets its item
+// word without kFresh (the other streams were never written for it).
 __device__ __forceinline__ void store_ray_v(const Queue& q, int32_t i, pt_v3 o, pt_v3 d, pt_v3 thr, uint32_t item,
-                                            uint32_t ctr, uint32_t meta) {
+                                            bool was_fresh, uint32_t ctr, uint32_t meta) {
   s_store((pt_qf4*)(q.a + i), pt_qf4{o.x, o.y, o.z, d.x});
-  s_store((pt_qf4*)(q.b + i), pt_qf4{d.y, d.z, __uint_as_float(item), __uint_as_float(ctr)});
+  s_store((pt_qf2*)(q.d + i), pt_qf2{d.y, d.z});
   s_store((pt_qf4*)(q.c + i), pt_qf4{thr.x, thr.y, thr.z, __uint_as_float(meta)});
+  s_store(q.ctr + i, ctr);
+  if (was_fresh) s_store(q.item + i, item);
 }
 
-// The slot's state lives in its work-item word (B.z): an item, kPending or kDead.
-__device__ __forceinline__ void set_slot_item(const Queue& q, int32_t i, uint32_t v) {
-  s_store(reinterpret_cast<uint32_t*>(q.b + i) + 2, v);
-}
+// The slot's state lives in its work-item word: an item (| kFresh), kPending or kDead.
+__device__ __forceinline__ void set_slot_item(const Queue& q, int32_t i, uint32_t v) { s_store(q.item + i, v); }
 
-__device__ __forceinline__ uint32_t slot_item(const Queue& q, int32_t i) {
-  return s_load(reinterpret_cast<const uint32_t*>(q.b + i) + 2);
-}
-
-__device__ __forceinline__ Ray load_ray(const Queue& q, int32_t i) {
-  float4 a = q_load(q.a + i), b = q_load(q.b + i), c = q_load(q.c + i);
-  Ray r;
-  r.o = pt_v3f(a.x, a.y, a.z);
-  r.d = pt_v3f(a.w, b.x, b.y);
-  r.item = __float_as_uint(b.z);
-  r.ctr = __float_as_uint(b.w);
-  r.thr = pt_v3f(c.x, c.y, c.z);
-  r.meta = __float_as_uint(c.w);
-  return r;
-}
+__device__ __forceinline__ uint32_t slot_item(const Queue& q, int32_t i) { return s_load(q.item + i); }
 
 // Work items come in chunks of one 8x8 pixel square x csamp samples. Chunk c
 // is square c % nsq of sample block c / nsq (so early chunks cover every
@@ -308,6 +311,36 @@ __device__ __forceinline__ Item decode_item(const DevFrame& fr, const WfBufs& wb
 
 __device__ __forceinline__ uint32_t path_key(const DevFrame& fr, const WfBufs& wb, const Item& it) {
   return pt_path_key(fr.seed, (uint32_t)(it.py * fr.width + it.px), (uint32_t)(wb.s_begin + it.srel));
+}
+
+// The ray of slot i for wf_scatter, with its decoded work item. A fresh
+// camera ray (generated and traced in this iteration's wf_intersect, not
+// stored) is regenerated from its item: the same get_ray draws
+// (kernels.py:1219-1239, direction unnormalized, Q1), throughput 1, depth and
+// wave 0.
+__device__ __forceinline__ Ray load_ray(const DevFrame& fr, const WfBufs& wb, int32_t i, Item& it) {
+  const Queue& q = wb.q;
+  Ray r;
+  const uint32_t w = s_load(q.item + i);
+  r.fresh = (w & kFresh) != 0u;
+  r.item = w & ~kFresh;
+  it = decode_item(fr, wb, r.item);
+  if (r.fresh) {
+    Rng rng{path_key(fr, wb, it), 0u};
+    get_ray(fr, it.px, it.py, rng, r.o, r.d);
+    r.ctr = rng.n;
+    r.thr = pt_v3f(1.0f, 1.0f, 1.0f);
+    r.meta = 0u;
+  } else {
+    const float4 a = q_load(q.a + i), c = q_load(q.c + i);
+    const float2 d = h_load(q.d + i);
+    r.o = pt_v3f(a.x, a.y, a.z);
+    r.d = pt_v3f(a.w, d.x, d.y);
+    r.ctr = s_load(q.ctr + i);
+    r.thr = pt_v3f(c.x, c.y, c.z);
+    r.meta = __float_as_uint(c.w);
+  }
+  return r;
 }
 
 
@@ -346,7 +379,7 @@ __device__ __forceinline__ int2 fetch_units(const WfBufs& wb, int32_t shard) {
 // starts at its first unit.
 __global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb, int32_t init_next) {
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kWfBlock)) {
-    reinterpret_cast<uint32_t*>(wb.q.b + i)[2] = kPending;
+    wb.q.item[i] = kPending;
     if ((i & 63) == 0) wb.grp[i >> 6] = make_int2(0, 0);
   }
   if (init_next && blockIdx.x < kShards && threadIdx.x == 0) {
@@ -359,8 +392,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb, 
 // Hand the group's (this wave's) next items to its slots waiting for work,
 // taking a new chunk when the current one runs out; slots that find no work
 // retire. Wave-uniform: called by all 64 lanes of the group. A slot given a
-// camera ray gets its origin and direction in (o, d) too (true returned; its
-// throughput is 1), so the caller need not read back what was just stored.
+// camera ray gets its origin and direction in (o, d) (true returned); only
+// its item word is stored, marked kFresh (wf_scatter regenerates the ray).
 __device__ __forceinline__ bool assign_work(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& item,
                                             pt_v3& o, pt_v3& d) {
   const bool pending = item == kPending;
@@ -402,8 +435,8 @@ __device__ __forceinline__ bool assign_work(const DevFrame& fr, const WfBufs& wb
       const Item it = decode_item(fr, wb, my);
       Rng rng{path_key(fr, wb, it), 0u};
       get_ray(fr, it.px, it.py, rng, o, d);
-      store_ray_v(wb.q, i, o, d, pt_v3f(1.0f, 1.0f, 1.0f), my, rng.n, 0u);
-      item = my;
+      item = my | kFresh;
+      set_slot_item(wb.q, i, item);
       fresh = true;
     }  // an item outside the frame / batch: the slot stays pending
   }
@@ -426,12 +459,16 @@ __device__ __forceinline__ void end_path(const DevFrame& fr, const WfBufs& wb, i
 // of table round trips into every Lambertian wave that holds it.
 static_assert(PTMI_CLASS_LAMBERTIAN == kListLambertian && PTMI_CLASS_GLOSSY == kListGlossy &&
                   PTMI_CLASS_DIELECTRIC == kListDielectric && PTMI_CLASS_MEDIUM == kListMedium &&
-                  PTMI_CLASS_NOISE == kListNoise,
+                  PTMI_CLASS_NOISE == kListNoise && PTMI_CLASS_EMISSIVE == kListEnded,
               "leaf classes are list ids");
 
 // intersect_rays, kernels.py:1242-1263, plus the closest-hit classification:
-// shade_miss_rays (kernels.py:1266-1280) and emissive hits end their paths
-// here; every other traced slot is appended to its material's list.
+// every traced slot is appended to the list of its hit's material class, a
+// miss (shade_miss_rays, kernels.py:1266-1280) and an emissive hit
+// (kernels.py:1365-1375) to the ended list. Its streams: the item word of
+// every slot, o and d of a traced one (24 B), the hit record (8 B) and one
+// list entry (4 B) written; nothing else (a fresh camera ray is not stored,
+// path ends are staged by wf_scatter).
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
@@ -440,13 +477,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid, wb.spill, (uint32_t)(blockIdx.x * kWfBlock + tid) * 8u, gridDim.x * kWfBlock * 8u};
   const Queue q = wb.q;
-  const pt_v3 bg = pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]);
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
-  uint32_t n_live = 0, n_ended = 0;
+  uint32_t n_live = 0;
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + tid); i < wb.capacity; i += stride) {
-    const float4 b = q_load(q.b + i);
-    uint32_t item = __float_as_uint(b.z);
+    uint32_t item = s_load(q.item + i);
     pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
     // generate_camera_rays (kernels.py:1219-1239) for slots that need work
     const bool fresh = assign_work(fr, wb, i, item, o, d);
@@ -455,33 +490,16 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
       ++n_live;
       if (!fresh) {
         const float4 a = q_load(q.a + i);
+        const float2 dyz = h_load(q.d + i);
         o = pt_v3f(a.x, a.y, a.z);
-        d = pt_v3f(a.w, b.x, b.y);
+        d = pt_v3f(a.w, dyz.x, dyz.y);
       }
-      float t;
-      int32_t ref;
+      float t = 0.0f;
+      int32_t ref = 0;
       const bool hit = traverse<STACK, kWfBlock, TRAV, LDS>(sc, o, d, kTMin, kTMax, st, t, ref);
-      if (hit) {
-        list = leaf_class(ref);
-        h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
-      }
-      if (!hit || list == PTMI_CLASS_EMISSIVE) {
-        // a miss (thr * bg) or an emissive hit (thr * emit, if any), then the path ends
-        pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);  // a fresh camera ray's
-        if (!fresh) {
-          const float4 c = q_load(q.c + i);
-          thr = pt_v3f(c.x, c.y, c.z);
-        }
-        pt_v3 col = pt_mul(thr, bg);
-        if (hit) {
-          const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
-          col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z))
-                                                         : pt_v3f(0.0f, 0.0f, 0.0f);
-        }
-        end_path(fr, wb, i, item, col);
-        ++n_ended;
-        list = -1;
-      }
+      if (!hit) ref = 0;  // a miss: no leaf code
+      list = hit ? leaf_class(ref) : kListEnded;
+      h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
     }
     // wave-uniform appends, one atomic per wave and non-empty list; lane 0
     // issues them all before it waits for any (independent round trips)
@@ -515,10 +533,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
       if (k < wb.medseg) s_store(list_slot(wb, list, shard, k), i);  // always true: a shard has medseg slots
     }
   }
-  if (counters) {
-    block_flush<1>({n_live}, lds_stack, counters + 0);
-    block_flush<1>({n_ended}, lds_stack, counters + 2);
-  }
+  if (counters) block_flush<1>({n_live}, lds_stack, counters + 0);
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
@@ -548,14 +563,14 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, const WfBuf
     ++ends[1];
     return false;
   }
-  store_ray_v(wb.q, i, hp, sdir, nthr, cur.item, r.n, (uint32_t)nd | ((uint32_t)(wave + 1) << 8));
+  store_ray_v(wb.q, i, hp, sdir, nthr, cur.item, cur.fresh, r.n, (uint32_t)nd | ((uint32_t)(wave + 1) << 8));
   return true;
 }
 
-// Per-lane tail of wf_scatter for a path that ended: stage its
-// colour (0 unless it ended on an emissive boundary fallback; emissive
-// surface hits end in wf_intersect) and mark the slot as waiting for work (the
-// next wf_intersect hands it the next item).
+// Per-lane tail of wf_scatter for a path a scatter ended: stage its colour
+// (0 unless it ended on an emissive boundary fallback; misses and emissive
+// surface hits come through the ended list, ended_entry) and mark the slot as
+// waiting for work (the next wf_intersect hands it the next item).
 __device__ __forceinline__ void finish_ended(const DevFrame& fr, const WfBufs& wb, int32_t i, const Ray& ray,
                                              pt_v3 emit) {
   end_path(fr, wb, i, ray.item,
@@ -586,15 +601,38 @@ __device__ __forceinline__ int32_t list_counts(const WfBufs& wb, int32_t par, in
   return n;
 }
 
+// One entry i of the ended list: a miss (thr * background, shade_miss_rays
+// kernels.py:1266-1280) or an emissive surface hit (thr * emit when the emit
+// colour is non-zero, kernels.py:1365-1375); the path ends without a scatter.
+// A fresh camera ray's throughput is 1 (its ray is not regenerated: nothing
+// else of it is needed).
+__device__ __forceinline__ void ended_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t i,
+                                            uint32_t& n_ended) {
+  const int32_t ref = __float_as_int(h_load(wb.hit + i).y);
+  const uint32_t w = s_load(wb.q.item + i);
+  pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);
+  if (!(w & kFresh)) {
+    const float4 c = q_load(wb.q.c + i);
+    thr = pt_v3f(c.x, c.y, c.z);
+  }
+  pt_v3 col = pt_mul(thr, pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]));
+  if (ref != 0) {
+    const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
+    col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z)) : pt_v3f(0.0f, 0.0f, 0.0f);
+  }
+  end_path(fr, wb, i, w & ~kFresh, col);
+  ++n_ended;
+}
+
 // One entry i of the Lambertian, glossy or dielectric list (`list`,
 // wave-uniform): shade_and_scatter for a surface hit (kernels.py:1359-1399).
 __device__ __forceinline__ void shade_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t list,
                                             int32_t i, uint32_t& n_ended, uint32_t (&ends)[2]) {
   const float2 h = h_load(wb.hit + i);
   const int32_t ref = __float_as_int(h.y);
-  const Ray ray = load_ray(wb.q, i);
+  Item it;
+  const Ray ray = load_ray(fr, wb, i, it);
   const Mat m = load_mat(sc, mat_index(sc, ref));
-  Item it = decode_item(fr, wb, ray.item);
   Rng r{path_key(fr, wb, it), ray.ctr};
   const pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
   const pt_v3 nrm = hit_normal(sc, ref, hp, ray.d);
@@ -625,14 +663,14 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
   pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
   const float2 h = h_load(wb.hit + i);
   const int32_t ref = __float_as_int(h.y);
-  const Ray ray = load_ray(wb.q, i);
+  Item it;
+  const Ray ray = load_ray(fr, wb, i, it);
   float te = 0.0f;
   int32_t rex = 0;
   bool hx = false;
   if (!is_noise)  // the exit search from t_entry + 1e-4 (kernels.py:417-419)
     hx = traverse<STACK, kWfBlock, TRAV>(sc, ray.o, ray.d, h.x + 0.0001f, kTMax, st, te, rex);
   const Mat m = load_mat(sc, mat_index(sc, ref));
-  Item it = decode_item(fr, wb, ray.item);
   Rng r{path_key(fr, wb, it), ray.ctr};
   bool surface = is_noise, scattered = false, passthrough = false;
   int32_t ruv = kRuvNone;
@@ -652,8 +690,8 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
         ++ends[1];  // Q14: no wave left for the passthrough
       } else {
         float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
-        store_ray_v(wb.q, i, pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t)), ray.d, ray.thr, ray.item, r.n,
-                    ray.meta + (1u << 8));
+        store_ray_v(wb.q, i, pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t)), ray.d, ray.thr, ray.item, ray.fresh,
+                    r.n, ray.meta + (1u << 8));
         go = true;
       }
     } else {  // fallback: the boundary as a surface (kernels.py:1352-1357)
@@ -702,7 +740,8 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
-  constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
+  constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric,
+                                      kListEnded};
   int32_t cnt[kLists][kShards], num[kLists], span[kLists];  // wave-uniform
   int32_t n = 0;
 #pragma unroll
@@ -731,9 +770,63 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
       if (l == k && j < num[k]) i = list_entry(wb, kOrder[k], cnt[k], j);
     if (i < 0) continue;  // the list's padding
     if (l < 2) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, l == 1, n_ended, ends);
+    else if (l == kLists - 1) ended_entry(sc, fr, wb, i, n_ended);
     else shade_entry(sc, fr, wb, kOrder[l], i, n_ended, ends);  // kOrder[l] for l = 2, 3, 4: selects
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
+}
+
+// The tail of a batch (wf_batch switches a pipe to it once its live slots fall
+// below PTMI_WF_DRAIN_AT of its capacity, i.e. after the work pool ran dry):
+// one launch finishes every path still in the pipe, each lane looping
+// intersect -> classify -> shade over its own slot until the path ends —
+// exactly the per-path steps of wf_intersect and wf_scatter (the same entry
+// functions, reading and writing the same slot), so every path, its draws,
+// its wave budget (Q14) and the counters are unchanged. What changes is the
+// schedule: instead of one intersect and one scatter launch per remaining
+// wave (~7.5 us each even when nearly empty, and ~50 of them for the longest
+// Russian-roulette survivors), the tail is one launch whose length is the
+// longest remaining path. Launched on the pipe's stream after a wf_scatter,
+// so no slot is fresh and the lists are not used; a pending slot finds no
+// work (the pool is empty) and is left alone.
+template <int STACK, int TRAV = PTMI_TRAV_STACK>
+__global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, WfBufs wb,
+                                                   unsigned long long* __restrict__ counters) {
+  __shared__ uint2 lds_stack[STACK * kWfBlock];
+  Stack st{lds_stack + threadIdx.x};
+  const Queue q = wb.q;
+  uint32_t n_seg = 0, n_med = 0, n_ended = 0, ends[2] = {0u, 0u};
+  for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity;
+       i += (int32_t)(gridDim.x * kWfBlock)) {
+    if (s_load(q.item + i) >= kPending) continue;  // retired, or waiting for work the pool no longer has
+    for (;;) {
+      // intersect_rays (kernels.py:1242-1263) for this slot
+      const float4 a = q_load(q.a + i);
+      const float2 dyz = h_load(q.d + i);
+      float t = 0.0f;
+      int32_t ref = 0;
+      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, pt_v3f(a.x, a.y, a.z), pt_v3f(a.w, dyz.x, dyz.y), kTMin,
+                                                       kTMax, st, t, ref);
+      ++n_seg;
+      if (!hit) ref = 0;
+      h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
+      const int32_t list = hit ? leaf_class(ref) : kListEnded;
+      const uint32_t before = n_ended;
+      if (list == kListEnded) {
+        ended_entry(sc, fr, wb, i, n_ended);
+      } else if (list == kListMedium || list == kListNoise) {
+        n_med += list == kListMedium ? 1u : 0u;
+        medium_entry<STACK, TRAV>(sc, fr, wb, st, i, list == kListNoise, n_ended, ends);
+      } else {
+        shade_entry(sc, fr, wb, list, i, n_ended, ends);
+      }
+      if (n_ended != before) break;  // the path ended; its slot waits for work that will not come
+    }
+  }
+  if (counters) {
+    block_flush<2>({n_seg, n_med}, lds_stack, counters + 0);
+    block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
+  }
 }
 
 namespace {
@@ -773,12 +866,19 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
 #ifndef PTMI_WF_RB_CHUNK
 #define PTMI_WF_RB_CHUNK 8
 #endif
+#ifndef PTMI_WF_DRAIN_AT
+// A pipe whose read-back live count falls below capacity / PTMI_WF_DRAIN_AT
+// finishes its paths in one wf_drain launch (0 = never: one intersect and one
+// scatter launch per wave until the pipe is empty).
+#define PTMI_WF_DRAIN_AT 16
+#endif
 #ifndef PTMI_WF_CAPACITY_LOG2
 #define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
 #endif
 constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
 constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
+constexpr size_t kQueueBytesPerSlot = 48;
 struct Layout {
   int32_t capacity, medseg;
   size_t q, hit, lists, grp, staging, spill, ctl, total;
@@ -794,8 +894,8 @@ Layout layout(int32_t npix, int32_t batch) {
   L.capacity = (int32_t)cap;  // all pipes; each pipe has capacity / kPipes slots
   L.medseg = (int32_t)(cap / kPipes / kShards);
   size_t c = (size_t)cap;
-  L.q = 0;
-  L.hit = L.q + 3 * sizeof(float4) * c;
+  L.q = 0;  // queue streams: A (16 B), D (8 B), C (16 B), item (4 B), ctr (4 B) per slot
+  L.hit = L.q + kQueueBytesPerSlot * c;
   L.lists = L.hit + sizeof(float2) * c;
   L.grp = (L.lists + 4 * sizeof(int32_t) * c + 15) & ~(size_t)15;
   L.staging = (L.grp + sizeof(int2) * (c / 64) + 15) & ~(size_t)15;
@@ -883,11 +983,25 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     if (err != hipSuccess) break;
     if (!waited) continue;  // first chunk: nothing read back yet
     bool any = false;
-    for (int p = 0; p < kPipes; ++p) {
-      if (inflight[prev][p]) live[p] = live[p] && ps.pinned_live[prev * kPipes + p] != 0;
+    for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
+      if (inflight[prev][p]) {
+        const int32_t n_live = ps.pinned_live[prev * kPipes + p];
+        live[p] = live[p] && n_live != 0;
+        if (live[p] && PTMI_WF_DRAIN_AT > 0 && (int64_t)n_live * PTMI_WF_DRAIN_AT < (int64_t)wbs[p].capacity) {
+          // the pool is empty (some slot found no work) and few paths are left:
+          // finish them in one launch, queued behind the iterations in flight
+          const int pd = prof_begin(kProfWfDrain, st[p]);
+          hipLaunchKernelGGL((wf_drain<STACK, TRAV>), dim3((unsigned)(wbs[p].capacity / kWfBlock)), dim3(kWfBlock), 0,
+                             st[p], sc, fr, wbs[p], counters);
+          prof_end(pd, st[p]);
+          err = hipGetLastError();
+          live[p] = false;
+        }
+      }
       inflight[prev][p] = false;
       any = any || live[p];
     }
+    if (err != hipSuccess) break;
     if (!any) break;
   }
   // the last chunk's readbacks may still be in flight: finish them before the
@@ -947,8 +1061,10 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     for (int p = 0; p < kPipes; ++p) {
       WfBufs& wb = wbs[p];
       wb.q.a = (float4*)(base + L.q) + p * cp;
-      wb.q.b = (float4*)(base + L.q + sizeof(float4) * c) + p * cp;
-      wb.q.c = (float4*)(base + L.q + 2 * sizeof(float4) * c) + p * cp;
+      wb.q.d = (float2*)(base + L.q + 16 * c) + p * cp;
+      wb.q.c = (float4*)(base + L.q + 24 * c) + p * cp;
+      wb.q.item = (uint32_t*)(base + L.q + 40 * c) + p * cp;
+      wb.q.ctr = (uint32_t*)(base + L.q + 44 * c) + p * cp;
       wb.hit = (float2*)(base + L.hit) + p * cp;
       wb.lists = (int32_t*)(base + L.lists) + p * 4 * cp;
       wb.grp = (int2*)(base + L.grp) + p * (cp / 64);
@@ -977,7 +1093,8 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     else if (stack_needed <= 20) e = wf_batch<20>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 24) e = wf_batch<24>(sc, fr, wbs, accum, nb, counters, stream, *ps);
     else if (stack_needed <= 32) e = wf_batch<32>(sc, fr, wbs, accum, nb, counters, stream, *ps);
-    else e = wf_batch<64>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else if (stack_needed <= kRefStackSlots - 1) e = wf_batch<64>(sc, fr, wbs, accum, nb, counters, stream, *ps);
+    else e = wf_batch<kRefStackSlots, kTravRefStack>(sc, fr, wbs, accum, nb, counters, stream, *ps);  // leaf depth > 62
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -57,7 +57,7 @@ EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_rende
            'ptmi_mk_render_ws', 'ptmi_mk_trace_ws', 'ptmi_mk_max_batch', 'ptmi_mk_resolve_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
            'ptmi_prof_stop', 'ptmi_prof_stop_busy', 'ptmi_node_bytes')
-PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'retired', 'wf_scatter', 'wf_resolve', 'mk_resolve')
+PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_drain', 'wf_scatter', 'wf_resolve', 'mk_resolve')
 
 _lib = None
 

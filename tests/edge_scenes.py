@@ -6,7 +6,15 @@
   (every internal node has a leaf left child and an internal right child), so
   the deepest leaf sits at depth N-1 and the integrator must dispatch its 17-
   to 20-slot (N = 17..20) or 24-, 32- or 64-slot traversal kernels, most of
-  which the BASELINE scenes (leaf depth <= 16) never reach. The flattened arrays follow the reference's layout
+  which the BASELINE scenes (leaf depth <= 16) never reach.
+* ``chainx<N>``: the same spheres seen along -x from the chain's +x end, with
+  the linear BVH's leaves ordered by x, far (-x) end first, and the ground
+  sphere deepest. Each internal node's box then projects nearer than its leaf
+  child, so the reference's stack (kernels.py:705-732) keeps one far leaf per
+  level and, past 64 entries, drops the pushes (kernels.py:719-740): for N > 64
+  the deep end of the chain (the near spheres and the ground) is never
+  visited. The overflow semantics the integrators must reproduce (leaf depth
+  N - 1 > 62). The flattened arrays follow the reference's layout
   (sah_bvh_builder.py:338-418 flatten: preorder, left child at i + 1, node
   box = union of the children's boxes, internal prim_type/prim_idx = -1).
 """
@@ -21,13 +29,13 @@ from ptmi.scenes import _wrap
 BG = (0.6, 0.7, 0.9)
 
 
-def _camera(width):
+def _camera(width, along_x=False):
     cam = camera()
     cam.aspect_ratio = 16.0 / 9.0
     cam.img_width = width
     cam.vfov = 40
-    cam.lookfrom = point3(0, 1.5, 8)
-    cam.lookat = point3(0, 0.2, 0)
+    cam.lookfrom = point3(12, 0.8, 0.5) if along_x else point3(0, 1.5, 8)
+    cam.lookat = point3(-4, 0, -1) if along_x else point3(0, 0.2, 0)
     cam.vup = vec3(0, 1, 0)
     cam.initialize()
     return sd.camera_upload(cam)
@@ -43,11 +51,13 @@ def _row(n):
     return w
 
 
-def _linear_bvh(sa):
+def _linear_bvh(sa, order=None):
     """Reference-layout flattened arrays of a linear BVH over the scene's
-    spheres (leaf i = sphere i, the last internal node holds the last two)."""
+    spheres (leaf i = sphere order[i], default sphere i; the last internal
+    node holds the last two)."""
     ns = sa.num_spheres
     assert ns >= 2 and sa.num_quads == 0 and sa.num_triangles == 0
+    order = np.arange(ns) if order is None else np.asarray(order)
     c = sa.sphere_data[:, :3].astype(np.float32)
     r = sa.sphere_data[:, 3:4].astype(np.float32)
     lo, hi = c - r, c + r  # sphere bbox as the reference computes it (hittable.py: center -/+ radius)
@@ -67,11 +77,11 @@ def _linear_bvh(sa):
         right[node] = node + 2
         parent[leaf] = node
         parent[node + 2] = node
-        ptype[leaf], pidx[leaf] = sd.PRIM_SPHERE, k
-        bmin[leaf], bmax[leaf] = lo[k], hi[k]
+        ptype[leaf], pidx[leaf] = sd.PRIM_SPHERE, order[k]
+        bmin[leaf], bmax[leaf] = lo[order[k]], hi[order[k]]
     last = n - 1
-    ptype[last], pidx[last] = sd.PRIM_SPHERE, ns - 1
-    bmin[last], bmax[last] = lo[ns - 1], hi[ns - 1]
+    ptype[last], pidx[last] = sd.PRIM_SPHERE, order[ns - 1]
+    bmin[last], bmax[last] = lo[order[ns - 1]], hi[order[ns - 1]]
     for k in range(ns - 2, -1, -1):  # unions bottom-up
         node = 2 * k
         bmin[node] = np.minimum(bmin[left[node]], bmin[right[node]])
@@ -98,9 +108,15 @@ def edge_scene(name, width=96):
         w.add(Sphere.stationary(point3(0, 0.3, 0), 1.2, lambertian.from_color(color(0.7, 0.3, 0.2))))
         sa = sd.compile_world(_wrap(w.objects))
     elif name.startswith('chain'):
-        sa = sd.compile_world(_wrap(_row(int(name[5:]) - 1).objects))  # + the ground sphere
-        sa.bvh = _linear_bvh(sa)
+        n = int(name[6:] if name.startswith('chainx') else name[5:])
+        sa = sd.compile_world(_wrap(_row(n - 1).objects))  # + the ground sphere
+        order = None
+        if name.startswith('chainx'):  # leaves by x ascending (far to near), the ground sphere deepest
+            small = sa.sphere_data[:, 3] < 50
+            order = np.concatenate([np.flatnonzero(small)[np.argsort(sa.sphere_data[small, 0], kind='stable')],
+                                    np.flatnonzero(~small)])
+        sa.bvh = _linear_bvh(sa, order)
     else:
         raise KeyError(name)
-    _cache[key] = (sa, _camera(width), BG)
+    _cache[key] = (sa, _camera(width, along_x=name.startswith('chainx')), BG)
     return _cache[key]

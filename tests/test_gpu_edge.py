@@ -5,6 +5,8 @@ C-ABI, against the CPU oracle, same bar as test_gpu_parity: per-pixel L-inf
 * an empty scene and a one-sphere scene (the BVH root is a leaf);
 * linear BVHs 21, 28 and 51 levels deep, which select the 24-, 32- and
   64-slot traversal kernels (the reference's 64-slot stack, kernels.py:719);
+* a linear BVH 69 levels deep whose walk overflows the reference's 64-entry
+  stack, so pushes are dropped (kernels.py:719-740): the reference-stack walk;
 * max_depth 1 and 2 (kernels.py:1139-1141 / 1383, SURVEY Q13/Q14);
 * a zero-sample call, which must leave the accumulator untouched;
 * 1x1, 3x1 and 13x7 frames (smaller than a wave or the pipes' work, ragged 8x8 squares).
@@ -73,6 +75,32 @@ def test_deep_bvh_uses_wider_stacks(name, variant):
     depth = sd.pack_device(edge_scene(name)[0]).max_leaf_depth
     assert depth + 1 > 20  # beyond the 16/20-slot kernels
     _check(name, variant, 4)
+
+
+@pytest.mark.parametrize('spp', [1, 4])
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_stack_overflow_drops_match_the_oracle(variant, spp):
+    """Leaf depth 69 (chainx70): the reference's 64-entry stack drops pushes
+    (kernels.py:719-740; tests/test_stack_overflow.py shows the drop changes
+    the image); both integrators run its exact walk (TravRS) and match the
+    oracle, direct (1 spp) and staged / wavefront (4 spp), counters included."""
+    import torch
+    from ptmi import device
+    from parity_helpers import compare
+    import oracle
+    sa, cam, bg = edge_scene('chainx70')
+    W, H = cam['width'], cam['height']
+    fr = oracle.make_frame(cam, bg, 50, 3, W, H)
+    ref = np.zeros((H, W, 3), np.float32)
+    ost = oracle.render(oracle.OracleScene(sa), fr, variant, ref, (0, 0, W, H), 0, spp, 0)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
+    integ.reset_counters()
+    (integ.render_mk if variant == 'mk' else integ.render_wf)(device.make_frame(cam, bg, 50, 3, W, H), acc, 0, spp)
+    torch.cuda.synchronize()
+    linf, exact = compare(acc.cpu().numpy(), ref, spp)
+    assert linf <= LINF_TOL and exact >= 0.999
+    assert integ.read_counters() == ost
 
 
 @pytest.mark.parametrize('name', ['chain17', 'chain18', 'chain19', 'chain20'])

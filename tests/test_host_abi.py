@@ -86,7 +86,14 @@ def test_scene_validation_errors():
     v.n_inner = 2
     v.max_leaf_depth = 63
     v.nodes = v.spheres = v.mats = v.perlin_vec = v.perlin_perm = 16
-    assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_ECAPACITY
+    v.num_bvh_nodes = 5
+    # leaf depth > 62 runs the reference's own 64-entry stack walk (its silent
+    # drops, kernels.py:719-740) on the reference-layout nodes: they must be bound
+    assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_EINVAL
+    assert 'ref_nodes' in lib.ptmi_last_error().decode()
+    v.ref_nodes = 32
+    assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_OK
+    v.ref_nodes = None
     v.max_leaf_depth = 2
     v.num_bvh_nodes = 4  # 3 primitives: 2N - 1 = 5 nodes
     assert lib.ptmi_scene_check(C.byref(v)) == _lib.PTMI_EINVAL

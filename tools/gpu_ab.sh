@@ -4,7 +4,13 @@
 set -u
 shopt -s nullglob
 mkdir -p gpurun_out
-libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so path-tracer-python_amd/ptmi/_lib/variants/*.so)
+# AB_VARIANTS="a b": only variants/libptmi_{a,b}.so (default: every variant)
+if [ -n "${AB_VARIANTS:-}" ]; then
+  libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so)
+  for n in $AB_VARIANTS; do libs+=(path-tracer-python_amd/ptmi/_lib/variants/libptmi_$n.so); done
+else
+  libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so path-tracer-python_amd/ptmi/_lib/variants/*.so)
+fi
 if [ "${AB_PARITY:-0}" = 1 ]; then
   for lib in "${libs[@]}"; do
     PTMI_LIB=$PWD/$lib timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x >> gpurun_out/ab_parity.log 2>&1

@@ -11,9 +11,13 @@
 #                A/B timing (tools/gpu_ab.sh) of every variants/*.so against
 #                the default build: wavefront on vol2 800x800 or the mesh-fog
 #                scene, megakernel on C2 / C4 / C5 shapes
+#                (WF_VARIANTS / MK_VARIANTS="a b": only variants/libptmi_{a,b}.so)
 #   parity_variants  the GPU parity tests against each variants/*.so
 #   cache_mk / cache_wf   L1/L2 hit-rate PMC pass of one 32-spp call (tools/pmc_cache_summary.py reads it)
 #   lat_mk / lat_wf       VALU / wait PMC passes (tools/gpu_pmc_latency.sh; tools/pmc_valu.py reads them)
+#   abtrace_<lib>_<mk|wf> rocprofv3 kernel trace + stats of tools/ab.py (64 spp x 2) with variants/libptmi_<lib>.so
+#                         (<lib> = default: the default build)
+#   abpmc_<lib>_<mk|wf>   FETCH_SIZE, WRITE_SIZE and cache-hit PMC passes of tools/ab.py (32 spp x 1), same libs
 #   probe                 the diagnostic probe builds (tools/gpu_probe.sh; variants libptmi_probe{1,2}.so)
 # Every step has its own time limit; the script stops at the first failure.
 set -u
@@ -39,16 +43,24 @@ for s in $STEPS; do
     fetch_*) c=${s#fetch_}; step $s 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch_$c -- python bench.py --preset $c --steps 4 --no-cpu-baseline ;;
     write_*) c=${s#write_}; step $s 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o write_$c -- python bench.py --preset $c --steps 4 --no-cpu-baseline ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 8 ;;
-    ab_wf_c3) step $s 900 env AB_MODES=wf bash tools/gpu_ab.sh ;;
-    ab_wf_fog) step $s 900 env AB_MODES=wf AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
-    ab_mk_c2) step $s 900 env AB_MODES=mk bash tools/gpu_ab.sh ;;
-    ab_mk_c4) step $s 900 env AB_MODES=mk AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
-    ab_mk_c5) step $s 900 env AB_MODES=mk AB_SCENE=vol2_final_scene_comparison AB_WIDTH=3840 AB_SPP=16 bash tools/gpu_ab.sh ;;
+    ab_wf_c3) step $s 900 env AB_MODES=wf AB_VARIANTS="${WF_VARIANTS:-}" bash tools/gpu_ab.sh ;;
+    ab_wf_fog) step $s 900 env AB_MODES=wf AB_VARIANTS="${WF_VARIANTS:-}" AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
+    ab_mk_c2) step $s 900 env AB_MODES=mk AB_VARIANTS="${MK_VARIANTS:-}" bash tools/gpu_ab.sh ;;
+    ab_mk_c4) step $s 900 env AB_MODES=mk AB_VARIANTS="${MK_VARIANTS:-}" AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
+    ab_mk_c5) step $s 900 env AB_MODES=mk AB_VARIANTS="${MK_VARIANTS:-}" AB_SCENE=vol2_final_scene_comparison AB_WIDTH=3840 AB_SPP=16 bash tools/gpu_ab.sh ;;
     parity_variants) for lib in path-tracer-python_amd/ptmi/_lib/variants/*.so; do
         step parity_$(basename $lib .so) 600 env PTMI_LIB=$PWD/$lib python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edge.py -x -q --timeout 300 --timeout-method thread; done ;;
     cache_mk|cache_wf) v=${s#cache_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_cache" -o $v -- python tools/ab.py $v 32 1 ;;
     lat_mk|lat_wf) v=${s#lat_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_$v bash tools/gpu_pmc_latency.sh ;;
     probe) step probe 600 bash tools/gpu_probe.sh ;;
+    abtrace_*) r=${s#abtrace_}; name=${r%_*}; mode=${r##*_}
+      lib=path-tracer-python_amd/ptmi/_lib/libptmi.so; [ "$name" = default ] || lib=path-tracer-python_amd/ptmi/_lib/variants/libptmi_$name.so
+      PTMI_LIB=$PWD/$lib step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/abtrace" -o ${name}_$mode -- python tools/ab.py $mode 64 2 ${AB_SCENE:-vol2_final_scene} ${AB_WIDTH:-800} ;;
+    abpmc_*) r=${s#abpmc_}; name=${r%_*}; mode=${r##*_}
+      lib=path-tracer-python_amd/ptmi/_lib/libptmi.so; [ "$name" = default ] || lib=path-tracer-python_amd/ptmi/_lib/variants/libptmi_$name.so
+      PTMI_LIB=$PWD/$lib step ${s}_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/abpmc" -o ${name}_${mode}_fetch -- python tools/ab.py $mode 32 1 &&
+      PTMI_LIB=$PWD/$lib step ${s}_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/abpmc" -o ${name}_${mode}_write -- python tools/ab.py $mode 32 1 &&
+      PTMI_LIB=$PWD/$lib step ${s}_cache 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/abpmc" -o ${name}_${mode}_cache -- python tools/ab.py $mode 32 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
