@@ -109,6 +109,12 @@ constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (
 // 176-201: the same draws from the same counter-based stream), with
 // throughput 1 and depth 0. Items are < 2^31 (wf_render bounds them).
 constexpr uint32_t kFresh = 0x80000000u;
+#ifndef PTMI_WF_FRESH_STORE
+// 1: wf_intersect stores a fresh camera ray's o, d and draw count (28 B) and
+// wf_scatter reads them back; 0: nothing but the item word is stored and
+// wf_scatter regenerates the ray (get_ray) from the item.
+#define PTMI_WF_FRESH_STORE 0
+#endif
 
 // Ray queue: five streams per slot, each read only by the stage that needs
 // it. wf_intersect reads the item word (4 B) of every slot and the ray
@@ -128,8 +134,17 @@ struct Queue {
 // Perlin; glossy and ended (misses and emissive hits: their paths end
 // without a scatter, shade_miss_rays kernels.py:1266-1280 and kernels.py:
 // 1365-1375).
+#ifndef PTMI_WF_END_IN_SCATTER
+// 0: wf_intersect ends misses and emissive hits itself (thr * bg / thr * emit
+// to the staging slot): its lanes that finish traversing early do it while
+// the wave's longest traversal runs, nearly for free. 1: they go to an ended
+// list that wf_scatter drains. A/B on MI355X (round 4, with the 24-B ray
+// reads): 1 costs wf_scatter +19 % time for wf_intersect -2.4 %, C3 -5 %
+// (profiles/r04/ab/).
+#define PTMI_WF_END_IN_SCATTER 0
+#endif
 enum : int32_t { kListLambertian = 0, kListGlossy = 1, kListDielectric = 2, kListMedium = 3, kListNoise = 4,
-                 kListEnded = 5, kLists = 6 };
+                 kListEnded = 5, kLists = PTMI_WF_END_IN_SCATTER ? 6 : 5 };
 
 struct WfBufs {
   Queue q;
@@ -326,9 +341,17 @@ __device__ __forceinline__ Ray load_ray(const DevFrame& fr, const WfBufs& wb, in
   r.item = w & ~kFresh;
   it = decode_item(fr, wb, r.item);
   if (r.fresh) {
+#if PTMI_WF_FRESH_STORE
+    const float4 a = q_load(q.a + i);
+    const float2 d = h_load(q.d + i);
+    r.o = pt_v3f(a.x, a.y, a.z);
+    r.d = pt_v3f(a.w, d.x, d.y);
+    r.ctr = s_load(q.ctr + i);
+#else
     Rng rng{path_key(fr, wb, it), 0u};
     get_ray(fr, it.px, it.py, rng, r.o, r.d);
     r.ctr = rng.n;
+#endif
     r.thr = pt_v3f(1.0f, 1.0f, 1.0f);
     r.meta = 0u;
   } else {
@@ -437,6 +460,13 @@ __device__ __forceinline__ bool assign_work(const DevFrame& fr, const WfBufs& wb
       get_ray(fr, it.px, it.py, rng, o, d);
       item = my | kFresh;
       set_slot_item(wb.q, i, item);
+#if PTMI_WF_FRESH_STORE
+      // the ray (A, D) and its draw count; throughput 1 and depth / wave 0 are
+      // implied by kFresh (no C record)
+      s_store((pt_qf4*)(wb.q.a + i), pt_qf4{o.x, o.y, o.z, d.x});
+      s_store((pt_qf2*)(wb.q.d + i), pt_qf2{d.y, d.z});
+      s_store(wb.q.ctr + i, rng.n);
+#endif
       fresh = true;
     }  // an item outside the frame / batch: the slot stays pending
   }
@@ -479,7 +509,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
   const Queue q = wb.q;
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
-  uint32_t n_live = 0;
+  uint32_t n_live = 0, n_ended = 0;
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + tid); i < wb.capacity; i += stride) {
     uint32_t item = s_load(q.item + i);
     pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
@@ -499,7 +529,27 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
       const bool hit = traverse<STACK, kWfBlock, TRAV, LDS>(sc, o, d, kTMin, kTMax, st, t, ref);
       if (!hit) ref = 0;  // a miss: no leaf code
       list = hit ? leaf_class(ref) : kListEnded;
-      h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
+#if !PTMI_WF_END_IN_SCATTER
+      if (list == kListEnded) {
+        // a miss (thr * bg, shade_miss_rays kernels.py:1266-1280) or an
+        // emissive hit (thr * emit, kernels.py:1365-1375): the path ends here
+        pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);  // a fresh camera ray's
+        if (!fresh) {
+          const float4 c = q_load(q.c + i);
+          thr = pt_v3f(c.x, c.y, c.z);
+        }
+        pt_v3 col = pt_mul(thr, pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]));
+        if (hit) {
+          const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
+          col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z))
+                                                         : pt_v3f(0.0f, 0.0f, 0.0f);
+        }
+        end_path(fr, wb, i, item & ~kFresh, col);
+        ++n_ended;
+        list = -1;
+      } else
+#endif
+        h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
     }
     // wave-uniform appends, one atomic per wave and non-empty list; lane 0
     // issues them all before it waits for any (independent round trips)
@@ -533,7 +583,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
       if (k < wb.medseg) s_store(list_slot(wb, list, shard, k), i);  // always true: a shard has medseg slots
     }
   }
-  if (counters) block_flush<1>({n_live}, lds_stack, counters + 0);
+  if (counters) {
+    block_flush<1>({n_live}, lds_stack, counters + 0);
+    if (!PTMI_WF_END_IN_SCATTER) block_flush<1>({n_ended}, lds_stack, counters + 2);
+  }
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
@@ -740,8 +793,12 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
+#if PTMI_WF_END_IN_SCATTER
   constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric,
                                       kListEnded};
+#else
+  constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
+#endif
   int32_t cnt[kLists][kShards], num[kLists], span[kLists];  // wave-uniform
   int32_t n = 0;
 #pragma unroll
@@ -770,7 +827,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
       if (l == k && j < num[k]) i = list_entry(wb, kOrder[k], cnt[k], j);
     if (i < 0) continue;  // the list's padding
     if (l < 2) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, l == 1, n_ended, ends);
-    else if (l == kLists - 1) ended_entry(sc, fr, wb, i, n_ended);
+    else if (PTMI_WF_END_IN_SCATTER && l == kLists - 1) ended_entry(sc, fr, wb, i, n_ended);
     else shade_entry(sc, fr, wb, kOrder[l], i, n_ended, ends);  // kOrder[l] for l = 2, 3, 4: selects
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
