@@ -114,6 +114,12 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_SHADE_DEFER_MAX 16
 #endif
 
+#ifndef PTMI_MK_ONE_RUV
+// One random_unit_vector call site per shading round (scatter_begin /
+// scatter_end, pt_device.hpp) for the medium scatter, metal fuzz and
+// isotropic, instead of three divergent copies of the rejection loop.
+#define PTMI_MK_ONE_RUV 0
+#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -348,6 +354,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   typename TravOf<TRAV>::T tr;
   tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
+  bool deferred = false;  // traced, its shading left for a later round (PTMI_MK_SHADE_DEFER)
   bool need_seg = false;  // begin a segment after this pass's refill
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
@@ -367,25 +374,15 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #if PTMI_MK_PRIO_TRAV >= 0
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
 #endif
-#if PTMI_MK_SHADE_DEFER
-    uint32_t run_kinds = (1u << kShadeKinds) - 1u;  // kinds shaded in this round
-#endif
     for (;;) {  // traversal steps
       // a lane's stack is empty unless its segment is mid-traversal (busy => trav)
       const unsigned long long mbusy = pt_ballot(tr.busy());
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-#if PTMI_MK_SHADE_DEFER
-      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) {
-        const bool fin = trav && !tr.busy();
-        const int32_t kind = shade_kind(ps.mode == kModeMediumExit, tr);
-        run_kinds = shade_round_kinds(fin, kind, nbusy);
-        if (pt_ballot(fin && ((run_kinds >> kind) & 1u)) != 0ull) break;
-      }
-#else
-      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
-#endif
+      // a round starts when a lane's segment has been traced since the last
+      // round (a deferred lane, PTMI_MK_SHADE_DEFER, waits for the next one)
+      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy() && !deferred) != 0ull) break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -414,9 +411,15 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
 #if PTMI_MK_SHADE_DEFER
-    // kinds of this round; after the loop ended with no lane traversing, all
-    if (pt_ballot(tr.busy()) == 0ull) run_kinds = (1u << kShadeKinds) - 1u;
-    const bool shade_now = trav && !tr.busy() && ((run_kinds >> shade_kind(ps.mode == kModeMediumExit, tr)) & 1u);
+    bool shade_now;
+    {  // the kinds this round shades (deferred lanes are re-evaluated too)
+      const bool fin = trav && !tr.busy();
+      const int32_t kind = shade_kind(ps.mode == kModeMediumExit, tr);
+      const unsigned long long mb = pt_ballot(tr.busy());
+      const uint32_t run = shade_round_kinds(fin, kind, __builtin_popcount((uint32_t)mb) + __builtin_popcount((uint32_t)(mb >> 32)));
+      shade_now = fin && ((run >> kind) & 1u);
+      deferred = fin && !shade_now;
+    }
 #else
     const bool shade_now = trav && !tr.busy();
 #endif
@@ -451,6 +454,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
         bool surface = !exit_mode;
         int32_t sref = ref;
         float st = t;
+        pt_v3 n = pt_v3f(0.0f, 0.0f, 0.0f);
+        int32_t ruv = kRuvNone;
+        (void)ruv;
         if (exit_mode) {
           ps.mode = kModeTrace;
           float t_exit;
@@ -458,7 +464,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           // apply_constant_medium, kernels.py:421-448 (density m3.w)
           if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
             hp = mp;  // kernels.py:1082-1097
+#if PTMI_MK_ONE_RUV
+            ruv = kRuvMedium;
+#else
             sdir = random_unit_vector(ps.rng);
+#endif
             att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
             scattered = true;
           } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
@@ -474,10 +484,21 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
         }
         if (surface) {  // kernels.py:1120-1128
           hp = pt_add(ps.o, pt_scale(ps.dir, st));
-          pt_v3 n = hit_normal(sc, sref, hp, ps.dir);
+          n = hit_normal(sc, sref, hp, ps.dir);
           ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
+#if PTMI_MK_ONE_RUV
+          ruv = scatter_begin(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att, scattered);
+#else
           scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
+#endif
         }
+#if PTMI_MK_ONE_RUV
+        if (ruv != kRuvNone) {  // one random_unit_vector site: medium, metal fuzz, isotropic
+          const pt_v3 v = random_unit_vector(ps.rng);
+          if (ruv == kRuvMedium) sdir = v;
+          else scattered = scatter_end(sc, ruv, sref, m, hp, n, v, sdir, att);
+        }
+#endif
       }
 
       if (!done && !to_medium) {
