@@ -67,15 +67,20 @@ enum {
  *             fields.py:52-63) for the stackless traversal
  *             (PTMI_TRAV_STACKLESS): {min.xyz, left | max.xyz, right |
  *             parent, leaf code (0 = internal), side, 0} (i32 bits), side = 0
- *             when the node is its parent's left child, else 1. May be NULL
- *             when no frame asks for the stackless traversal.
+ *             when the node is its parent's left child, else 1. Used by the
+ *             stackless traversal and by BVHs of leaf depth > 62 (the
+ *             reference's 64-entry stack walk); may be NULL otherwise.
  */
 typedef struct ptmi_scene_view {
     const float *nodes;
     int32_t n_inner;
     int32_t root_ref;          /* ref of the root (0 if internal) */
     float root_min[3], root_max[3];
-    int32_t max_leaf_depth;    /* root = 0; sizes the traversal stack */
+    int32_t max_leaf_depth;    /* root = 0; sizes the traversal stack. Past 62 the
+                                  kernels run the reference's own 64-entry stack
+                                  walk on ref_nodes (kernels.py:625-742, pushes
+                                  beyond 64 entries dropped), so ref_nodes must be
+                                  set (PTMI_EINVAL otherwise) */
     const float *spheres;
     const float *quads;
     const float *tris;
@@ -214,8 +219,9 @@ int ptmi_mk_resolve_ws(const ptmi_frame *frame, const void *workspace, size_t wo
  * and pinned readback slots are created under a per-device lock, and calls on
  * one device are serialised by that lock (calls on different devices run
  * concurrently). Launches go to the current HIP device, which must be the
- * device holding the pointers. Batches are capped at 2^31 - 1 (sample,
- * pixel) work items whatever the workspace size. */
+ * device holding the pointers. Batches are capped at 2^29 - 1 (sample,
+ * pixel) work items, padded to whole 8x8 squares and chunks, whatever the
+ * workspace size (the item word's top bits flag fresh camera rays). */
 size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
