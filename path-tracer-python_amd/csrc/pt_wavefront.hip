@@ -3,10 +3,12 @@
 // Replaces the wavefront stage kernels of kernels.py:1219-1418 as driven by
 // TaichiRenderer.render_wavefront (renderer.py:305-334). Stages and layout
 // are designed for CDNA4, not translated:
-//   * ray queue = three float4 streams per slot (A = o.xyz,d.x;
-//     B = d.yz, work item, rng draw counter; C = thr.xyz, meta) so every
-//     load/store is a 16-B-per-lane coalesced access; meta = depth | wave << 8.
-//     wf_intersect reads A and B only: the ray and its slot state in 32 B;
+//   * ray queue = five streams per slot (A = o.xyz,d.x; D = d.yz; C =
+//     thr.xyz, meta; the work-item word; the rng draw counter), each read
+//     only by the stage that needs it, every access a coalesced per-lane
+//     vector load/store; meta = depth | wave << 8. wf_intersect reads the
+//     item word and the ray (24 B); a fresh camera ray is not stored at all
+//     (wf_scatter regenerates it from its item);
 //   * hit record = 8 B (t, leaf ref); hit point and normal are recomputed in
 //     the shading kernel with the reference's own expressions;
 //   * CLOSEST-HIT CLASSIFICATION: wf_intersect ends the paths a hit or miss
@@ -43,6 +45,10 @@
 //     intersect -> scatter on its own stream, so
 //     the drain at the end of one pipe's launch is filled by another's (+21 %
 //     over one pipe).
+//   * THE TAIL: once a pipe's live count falls below capacity / 16 (the
+//     work pool is empty), one wf_drain launch finishes its remaining paths,
+//     each lane looping intersect -> shade over its own slot, instead of ~50
+//     nearly empty intersect + scatter launches;
 //   * The host learns that a pipe has drained from a 4-byte live count read
 //     back every 8 iterations, and waits for chunk k's counts only after
 //     chunk k + 1 is queued, so no pipe idles through the host round trip
@@ -109,12 +115,6 @@ constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (
 // 176-201: the same draws from the same counter-based stream), with
 // throughput 1 and depth 0. Items are < 2^31 (wf_render bounds them).
 constexpr uint32_t kFresh = 0x80000000u;
-#ifndef PTMI_WF_FRESH_STORE
-// 1: wf_intersect stores a fresh camera ray's o, d and draw count (28 B) and
-// wf_scatter reads them back; 0: nothing but the item word is stored and
-// wf_scatter regenerates the ray (get_ray) from the item.
-#define PTMI_WF_FRESH_STORE 0
-#endif
 
 // Ray queue: five streams per slot, each read only by the stage that needs
 // it. wf_intersect reads the item word (4 B) of every slot and the ray
@@ -128,23 +128,16 @@ struct Queue {
 };
 
 // Closest-hit lists (wf_intersect fills them, wf_scatter drains them).
-// Each list holds kShards segments of medseg slot indices. Two pairs of lists
-// share one array, the second filling its segments from the top (a slot is in
-// at most one list, so together they never exceed a segment): medium and
-// Perlin; glossy and ended (misses and emissive hits: their paths end
-// without a scatter, shade_miss_rays kernels.py:1266-1280 and kernels.py:
-// 1365-1375).
-#ifndef PTMI_WF_END_IN_SCATTER
-// 0: wf_intersect ends misses and emissive hits itself (thr * bg / thr * emit
-// to the staging slot): its lanes that finish traversing early do it while
-// the wave's longest traversal runs, nearly for free. 1: they go to an ended
-// list that wf_scatter drains. A/B on MI355X (round 4, with the 24-B ray
-// reads): 1 costs wf_scatter +19 % time for wf_intersect -2.4 %, C3 -5 %
-// (profiles/r04/ab/).
-#define PTMI_WF_END_IN_SCATTER 0
-#endif
+// Each list holds kShards segments of medseg slot indices; the medium and
+// Perlin lists share one array, the Perlin one filling its segments from the
+// top (a slot is in at most one list, so together they never exceed a segment).
+// Misses and emissive hits (class kListEnded) end in wf_intersect: a lane
+// that finishes its traversal early ends its path while the wave's longest
+// traversal runs, nearly for free. A/B on MI355X (round 4): an ended list
+// drained by wf_scatter instead cost wf_scatter +19 % for wf_intersect -2.4 %,
+// C3 -5 % (profiles/r04/ab/). kListEnded is a class, not a list.
 enum : int32_t { kListLambertian = 0, kListGlossy = 1, kListDielectric = 2, kListMedium = 3, kListNoise = 4,
-                 kListEnded = 5, kLists = PTMI_WF_END_IN_SCATTER ? 6 : 5 };
+                 kListEnded = 5, kLists = 5 };
 
 struct WfBufs {
   Queue q;
@@ -194,9 +187,9 @@ __host__ __device__ __forceinline__ int32_t* ctl_list(const WfBufs& wb, int32_t 
 }
 // slot-index entry k of shard s's segment of a list
 __device__ __forceinline__ int32_t* list_slot(const WfBufs& wb, int32_t list, int32_t s, int32_t k) {
-  const int32_t arr = list < kListMedium ? list : list == kListEnded ? kListGlossy : kListMedium;
+  const int32_t arr = list < kListMedium ? list : kListMedium;
   int32_t* seg = wb.lists + (size_t)arr * (size_t)wb.capacity + (size_t)s * (size_t)wb.medseg;
-  return (list == kListNoise || list == kListEnded) ? seg + wb.medseg - 1 - k : seg + k;
+  return list == kListNoise ? seg + wb.medseg - 1 - k : seg + k;
 }
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -341,17 +334,10 @@ __device__ __forceinline__ Ray load_ray(const DevFrame& fr, const WfBufs& wb, in
   r.item = w & ~kFresh;
   it = decode_item(fr, wb, r.item);
   if (r.fresh) {
-#if PTMI_WF_FRESH_STORE
-    const float4 a = q_load(q.a + i);
-    const float2 d = h_load(q.d + i);
-    r.o = pt_v3f(a.x, a.y, a.z);
-    r.d = pt_v3f(a.w, d.x, d.y);
-    r.ctr = s_load(q.ctr + i);
-#else
+    // (storing it in wf_intersect instead, 28 B, measured 1-2 % slower on C3)
     Rng rng{path_key(fr, wb, it), 0u};
     get_ray(fr, it.px, it.py, rng, r.o, r.d);
     r.ctr = rng.n;
-#endif
     r.thr = pt_v3f(1.0f, 1.0f, 1.0f);
     r.meta = 0u;
   } else {
@@ -460,13 +446,6 @@ __device__ __forceinline__ bool assign_work(const DevFrame& fr, const WfBufs& wb
       get_ray(fr, it.px, it.py, rng, o, d);
       item = my | kFresh;
       set_slot_item(wb.q, i, item);
-#if PTMI_WF_FRESH_STORE
-      // the ray (A, D) and its draw count; throughput 1 and depth / wave 0 are
-      // implied by kFresh (no C record)
-      s_store((pt_qf4*)(wb.q.a + i), pt_qf4{o.x, o.y, o.z, d.x});
-      s_store((pt_qf2*)(wb.q.d + i), pt_qf2{d.y, d.z});
-      s_store(wb.q.ctr + i, rng.n);
-#endif
       fresh = true;
     }  // an item outside the frame / batch: the slot stays pending
   }
@@ -481,6 +460,27 @@ __device__ __forceinline__ void end_path(const DevFrame& fr, const WfBufs& wb, i
   set_slot_item(wb.q, i, kPending);
 }
 
+// A path that ends without a scatter (its traced segment has class
+// kListEnded): a miss adds thr * background (shade_miss_rays, kernels.py:
+// 1266-1280), an emissive hit thr * emit when the emit colour is non-zero
+// (kernels.py:1365-1375). w = the slot's item word (a fresh camera ray's
+// throughput is 1: no C record was stored for it), ref = the hit's leaf code,
+// 0 for a miss.
+__device__ __forceinline__ void end_unscattered(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t i,
+                                                uint32_t w, int32_t ref) {
+  pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);
+  if (!(w & kFresh)) {
+    const float4 c = q_load(wb.q.c + i);
+    thr = pt_v3f(c.x, c.y, c.z);
+  }
+  pt_v3 col = pt_mul(thr, pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]));
+  if (ref != 0) {
+    const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
+    col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z)) : pt_v3f(0.0f, 0.0f, 0.0f);
+  }
+  end_path(fr, wb, i, w & ~kFresh, col);
+}
+
 // Closest-hit classes (PTMI_CLASS_*, include/ptmi.h) are packed into the
 // leaf codes by the host, so a hit's list is known without a material load.
 // Surface hits whose scatter evaluates Perlin turbulence (a noise texture on
@@ -493,12 +493,12 @@ static_assert(PTMI_CLASS_LAMBERTIAN == kListLambertian && PTMI_CLASS_GLOSSY == k
               "leaf classes are list ids");
 
 // intersect_rays, kernels.py:1242-1263, plus the closest-hit classification:
-// every traced slot is appended to the list of its hit's material class, a
-// miss (shade_miss_rays, kernels.py:1266-1280) and an emissive hit
-// (kernels.py:1365-1375) to the ended list. Its streams: the item word of
-// every slot, o and d of a traced one (24 B), the hit record (8 B) and one
-// list entry (4 B) written; nothing else (a fresh camera ray is not stored,
-// path ends are staged by wf_scatter).
+// a miss (shade_miss_rays, kernels.py:1266-1280) or an emissive hit
+// (kernels.py:1365-1375) ends its path here; every other traced slot is
+// appended to the list of its hit's material class. Its streams: the item
+// word of every slot, o and d of a traced one (24 B), the hit record (8 B)
+// and one list entry (4 B); a path end reads thr (16 B) and writes its
+// staging slot and item word. A fresh camera ray is not stored.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
@@ -529,27 +529,13 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
       const bool hit = traverse<STACK, kWfBlock, TRAV, LDS>(sc, o, d, kTMin, kTMax, st, t, ref);
       if (!hit) ref = 0;  // a miss: no leaf code
       list = hit ? leaf_class(ref) : kListEnded;
-#if !PTMI_WF_END_IN_SCATTER
       if (list == kListEnded) {
-        // a miss (thr * bg, shade_miss_rays kernels.py:1266-1280) or an
-        // emissive hit (thr * emit, kernels.py:1365-1375): the path ends here
-        pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);  // a fresh camera ray's
-        if (!fresh) {
-          const float4 c = q_load(q.c + i);
-          thr = pt_v3f(c.x, c.y, c.z);
-        }
-        pt_v3 col = pt_mul(thr, pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]));
-        if (hit) {
-          const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
-          col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z))
-                                                         : pt_v3f(0.0f, 0.0f, 0.0f);
-        }
-        end_path(fr, wb, i, item & ~kFresh, col);
+        end_unscattered(sc, fr, wb, i, item, ref);
         ++n_ended;
         list = -1;
-      } else
-#endif
+      } else {
         h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
+      }
     }
     // wave-uniform appends, one atomic per wave and non-empty list; lane 0
     // issues them all before it waits for any (independent round trips)
@@ -585,7 +571,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
   }
   if (counters) {
     block_flush<1>({n_live}, lds_stack, counters + 0);
-    if (!PTMI_WF_END_IN_SCATTER) block_flush<1>({n_ended}, lds_stack, counters + 2);
+    block_flush<1>({n_ended}, lds_stack, counters + 2);
   }
 }
 
@@ -622,7 +608,7 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, const WfBuf
 
 // Per-lane tail of wf_scatter for a path a scatter ended: stage its colour
 // (0 unless it ended on an emissive boundary fallback; misses and emissive
-// surface hits come through the ended list, ended_entry) and mark the slot as
+// surface hits end in wf_intersect, end_unscattered) and mark the slot as
 // waiting for work (the next wf_intersect hands it the next item).
 __device__ __forceinline__ void finish_ended(const DevFrame& fr, const WfBufs& wb, int32_t i, const Ray& ray,
                                              pt_v3 emit) {
@@ -654,28 +640,6 @@ __device__ __forceinline__ int32_t list_counts(const WfBufs& wb, int32_t par, in
   return n;
 }
 
-// One entry i of the ended list: a miss (thr * background, shade_miss_rays
-// kernels.py:1266-1280) or an emissive surface hit (thr * emit when the emit
-// colour is non-zero, kernels.py:1365-1375); the path ends without a scatter.
-// A fresh camera ray's throughput is 1 (its ray is not regenerated: nothing
-// else of it is needed).
-__device__ __forceinline__ void ended_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t i,
-                                            uint32_t& n_ended) {
-  const int32_t ref = __float_as_int(h_load(wb.hit + i).y);
-  const uint32_t w = s_load(wb.q.item + i);
-  pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);
-  if (!(w & kFresh)) {
-    const float4 c = q_load(wb.q.c + i);
-    thr = pt_v3f(c.x, c.y, c.z);
-  }
-  pt_v3 col = pt_mul(thr, pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]));
-  if (ref != 0) {
-    const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
-    col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z)) : pt_v3f(0.0f, 0.0f, 0.0f);
-  }
-  end_path(fr, wb, i, w & ~kFresh, col);
-  ++n_ended;
-}
 
 // One entry i of the Lambertian, glossy or dielectric list (`list`,
 // wave-uniform): shade_and_scatter for a surface hit (kernels.py:1359-1399).
@@ -793,12 +757,7 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
-#if PTMI_WF_END_IN_SCATTER
-  constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric,
-                                      kListEnded};
-#else
   constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
-#endif
   int32_t cnt[kLists][kShards], num[kLists], span[kLists];  // wave-uniform
   int32_t n = 0;
 #pragma unroll
@@ -827,7 +786,6 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
       if (l == k && j < num[k]) i = list_entry(wb, kOrder[k], cnt[k], j);
     if (i < 0) continue;  // the list's padding
     if (l < 2) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, l == 1, n_ended, ends);
-    else if (PTMI_WF_END_IN_SCATTER && l == kLists - 1) ended_entry(sc, fr, wb, i, n_ended);
     else shade_entry(sc, fr, wb, kOrder[l], i, n_ended, ends);  // kOrder[l] for l = 2, 3, 4: selects
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
@@ -870,7 +828,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, W
       const int32_t list = hit ? leaf_class(ref) : kListEnded;
       const uint32_t before = n_ended;
       if (list == kListEnded) {
-        ended_entry(sc, fr, wb, i, n_ended);
+        end_unscattered(sc, fr, wb, i, s_load(q.item + i), ref);
+        ++n_ended;
       } else if (list == kListMedium || list == kListNoise) {
         n_med += list == kListMedium ? 1u : 0u;
         medium_entry<STACK, TRAV>(sc, fr, wb, st, i, list == kListNoise, n_ended, ends);
