@@ -888,6 +888,9 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
 // scatter launch per wave until the pipe is empty).
 #define PTMI_WF_DRAIN_AT 16
 #endif
+#ifndef PTMI_WF_DRAIN_JOINT
+#define PTMI_WF_DRAIN_JOINT 0
+#endif
 #ifndef PTMI_WF_CAPACITY_LOG2
 #define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
 #endif
@@ -999,11 +1002,26 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     if (err != hipSuccess) break;
     if (!waited) continue;  // first chunk: nothing read back yet
     bool any = false;
+    // PTMI_WF_DRAIN_JOINT: every pipe drains once all of them together are
+    // below the threshold (the pipes share the work pool, so they run dry
+    // together; a pipe whose own count lags would otherwise drain a chunk or
+    // two after the others and set the call's end)
+    bool drain_all = false;
+    if (PTMI_WF_DRAIN_JOINT && PTMI_WF_DRAIN_AT > 0) {
+      int64_t n_sum = 0, cap_sum = 0;
+      for (int p = 0; p < kPipes; ++p)
+        if (inflight[prev][p] && live[p]) {
+          n_sum += ps.pinned_live[prev * kPipes + p];
+          cap_sum += wbs[p].capacity;
+        }
+      drain_all = cap_sum > 0 && n_sum * PTMI_WF_DRAIN_AT < cap_sum;
+    }
     for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
       if (inflight[prev][p]) {
         const int32_t n_live = ps.pinned_live[prev * kPipes + p];
         live[p] = live[p] && n_live != 0;
-        if (live[p] && PTMI_WF_DRAIN_AT > 0 && (int64_t)n_live * PTMI_WF_DRAIN_AT < (int64_t)wbs[p].capacity) {
+        if (live[p] && PTMI_WF_DRAIN_AT > 0 &&
+            (drain_all || (int64_t)n_live * PTMI_WF_DRAIN_AT < (int64_t)wbs[p].capacity)) {
           // the pool is empty (some slot found no work) and few paths are left:
           // finish them in one launch, queued behind the iterations in flight
           const int pd = prof_begin(kProfWfDrain, st[p]);

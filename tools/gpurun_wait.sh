@@ -4,7 +4,7 @@
 # off", a box lost while being prepared). A call that ran is never repeated.
 # Usage: tools/gpurun_wait.sh LOG TIMEOUT 'COMMAND'
 LOG=$1; T=$2; CMD=$3
-for try in 1 2 3 4 5 6 7 8; do
+for try in $(seq 1 ${GPURUN_TRIES:-20}); do
   timeout $((T + 900)) /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > "$LOG" 2>&1
   rc=$?
   if grep -q "status=transient" "$LOG" && grep -Eq "run (0.0|None)s of limit" "$LOG"; then
