@@ -288,3 +288,29 @@ def test_profiler_with_concurrent_megakernel_threads():
     mk, res = kt.result['megakernel'], kt.result['mk_resolve']
     assert mk['launches'] == n * calls == res['launches'] and not kt.truncated
     assert 0.0 < mk['busy_ms'] <= min(mk['ms'], wall_ms * 1.02 + 0.1)
+
+
+def test_wavefront_tail_runs_in_one_drain_launch_per_pipe():
+    """The wavefront's tail (wf_drain: once a pipe's live slots fall below
+    capacity / 16 after the work pool ran dry, one launch finishes its paths)
+    runs in every call that reaches it, and the render and the device counters
+    still equal the oracle's (the drain runs the same per-path entry
+    functions as wf_intersect / wf_scatter)."""
+    import torch
+    from parity_helpers import compare, oracle_render
+    from ptmi import device, _lib
+    sa, cam, bg = scene_inputs('vol2_final_scene', 800)
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    win = (336, 352, 96, 64)
+    fr = device.make_frame(cam, bg, 50, 0, cam['width'], cam['height'], win)
+    acc = torch.zeros((cam['height'], cam['width'], 3), dtype=torch.float32, device='cuda')
+    integ.reset_counters()
+    with _lib.KernelTimer(max_launches=100000) as kt:
+        integ.render_wf(fr, acc, 7, 8)
+        torch.cuda.synchronize()
+    drains = kt.result['wf_drain']['launches']
+    assert 1 <= drains <= 4  # at most one per pipe and batch
+    ref, ost = oracle_render('vol2_final_scene', 800, 'wf', win, 7, 8)
+    linf, exact = compare(acc.cpu().numpy(), ref, 8)
+    assert linf <= 1e-4 and exact >= 0.999
+    assert integ.read_counters() == ost
