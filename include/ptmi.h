@@ -219,9 +219,9 @@ int ptmi_mk_resolve_ws(const ptmi_frame *frame, const void *workspace, size_t wo
  * and pinned readback slots are created under a per-device lock, and calls on
  * one device are serialised by that lock (calls on different devices run
  * concurrently). Launches go to the current HIP device, which must be the
- * device holding the pointers. Batches are capped at 2^29 - 1 (sample,
+ * device holding the pointers. Batches are capped at 2^31 - 1 (sample,
  * pixel) work items, padded to whole 8x8 squares and chunks, whatever the
- * workspace size (the item word's top bits flag fresh camera rays). */
+ * workspace size (the item word's top bit flags a fresh camera ray). */
 size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,

@@ -21,9 +21,7 @@ constexpr float kTMax = 1e10f;
 constexpr int kRRMinDepth = 5;      // kernels.py:1050
 constexpr float kRRMaxProb = 0.95f; // kernels.py:1051
 constexpr int kNumCounters = PTMI_NUM_COUNTERS;  // include/ptmi.h
-#ifndef PTMI_ONE_TEXTURE_SITE
-#define PTMI_ONE_TEXTURE_SITE 0  // scatter(): one eval_texture call site for Lambertian and isotropic (A/B)
-#endif
+
 
 // n / d by one 64-bit multiply and shift: m = floor(2^(32+l) / d) + 1 with
 // 2^l >= d (so m <= 2^33) gives floor(n / d) exactly for every n < 2^32 in
@@ -937,22 +935,11 @@ __device__ __forceinline__ bool scatter(const DevScene& sc, int32_t ref, const M
   int32_t mt = m.mat_type();
   sdir = pt_v3f(0.0f, 0.0f, 0.0f);
   att = pt_v3f(1.0f, 1.0f, 1.0f);
-#if PTMI_ONE_TEXTURE_SITE
-  // one texture site for Lambertian and isotropic (eval_texture draws
-  // nothing, so evaluating it first keeps every draw in place): a shading
-  // round with both runs the texture code once, not twice
-  if (mt == 0 || mt == 4) att = eval_texture(sc, ref, m, hp);
-  if (mt == 0) {
-    sdir = random_cosine_direction(n, r);
-    return true;
-  }
-#else
   if (mt == 0) {
     att = eval_texture(sc, ref, m, hp);
     sdir = random_cosine_direction(n, r);
     return true;
   }
-#endif
   if (mt == 1) {
     pt_v3 refl = reflect3(pt_normalize(dir), n);
     sdir = pt_add(refl, pt_scale(random_unit_vector(r), m.m0.w));
@@ -968,9 +955,7 @@ __device__ __forceinline__ bool scatter(const DevScene& sc, int32_t ref, const M
   }
   if (mt == 4) {
     sdir = random_unit_vector(r);
-#if !PTMI_ONE_TEXTURE_SITE
     att = eval_texture(sc, ref, m, hp);
-#endif
     return true;
   }
   return false;  // emissive (3) and unknown types

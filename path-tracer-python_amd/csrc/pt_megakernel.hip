@@ -97,28 +97,18 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // +7.5 %, C5 +6.3 %, C4 +8 % with the shading threshold at 24 (0 = off).
 #define PTMI_MK_DEFER 12
 #endif
-#ifndef PTMI_MK_SHADE_DEFER
-// Shading-round deferral by material kind (0 = off). A shading round runs the
-// union of its lanes' material code, one branch after another for disjoint
-// lane sets (34 % of a wave's cycles on C2, profiles/r03/probe_r3.txt). With
-// deferral, a lane whose traced segment needs an expensive kind of shading
-// (medium free flight, Lambertian, Perlin, glossy, dielectric: shade_kind)
-// keeps its result and waits while fewer than PTMI_MK_SHADE_DEFER lanes of
-// the wave need the same kind, unless PTMI_MK_SHADE_DEFER_MAX lanes would be
-// left waiting or no lane is still traversing; cheap ends (a miss, a medium
-// boundary's mode switch, an emissive hit) shade at once. Each lane still
-// shades its own segments in its own order, so results are unchanged.
-#define PTMI_MK_SHADE_DEFER 0
-#endif
-#ifndef PTMI_MK_SHADE_DEFER_MAX
-#define PTMI_MK_SHADE_DEFER_MAX 16
-#endif
-
+// A/B, not kept (round 4): shading-round deferral by material kind (a lane
+// whose segment needs an expensive kind of shading waits until 4 / 8 / 12 /
+// 16 lanes need the same kind): C2 -0.5 %, C4 -1 %
+// (profiles/r04/ab/ab_r04i_split_knobs_ruv.log, ab_wf_layout_drain_mk_shade_defer.log).
 #ifndef PTMI_MK_ONE_RUV
 // One random_unit_vector call site per shading round (scatter_begin /
 // scatter_end, pt_device.hpp) for the medium scatter, metal fuzz and
-// isotropic, instead of three divergent copies of the rejection loop.
-#define PTMI_MK_ONE_RUV 0
+// isotropic, instead of three divergent copies of the rejection loop: the
+// loop then runs once, to the wave's longest lane. A/B on MI355X (round 4,
+// parity-identical): C4 +2.1 %, C2 +-0.3 % (profiles/r04/ab/ab_r04i_split_knobs_ruv.log;
+// round 2 measured C2 -1.1 % with the code of the time).
+#define PTMI_MK_ONE_RUV 1
 #endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
@@ -218,38 +208,6 @@ static int64_t mk_tiles(const DevFrame& fr, int32_t* tx_out = nullptr) {
   const int64_t tx = (fr.w + tw - 1) / tw, ty = (fr.n_rows + th - 1) / th;
   if (tx_out) *tx_out = (int32_t)tx;
   return tx * ty;
-}
-
-// Shading kind of a traced segment (PTMI_MK_SHADE_DEFER): 0 cheap (a miss, a
-// medium boundary's switch to the exit search, an emissive surface), 1 the
-// medium's free flight after its exit search, 2 Lambertian, 3 Perlin-textured,
-// 4 glossy (metal, isotropic, others), 5 dielectric. Surface kinds come from
-// the leaf code's material class (no load): classes 0..5 (PTMI_CLASS_*) map to
-// kinds 2, 4, 5, 0, 3, 0.
-constexpr int kShadeKinds = 6;
-template <class TR>
-__device__ __forceinline__ int32_t shade_kind(bool exit_mode, const TR& tr) {
-  constexpr uint32_t kKindOfClass = 2u | 4u << 3 | 5u << 6 | 0u << 9 | 3u << 12 | 0u << 15;
-  if (exit_mode) return 1;
-  if (!tr.any()) return 0;
-  return (int32_t)((kKindOfClass >> (3 * leaf_class(tr.best))) & 7u);
-}
-
-// Kinds the wave shades in this round (bit mask, wave-uniform), given which
-// lanes have a traced segment (fin) and its kind: cheap ends always; a kind
-// once PTMI_MK_SHADE_DEFER lanes have it; every kind when no lane is still
-// traversing or PTMI_MK_SHADE_DEFER_MAX lanes would be left waiting.
-__device__ __forceinline__ uint32_t shade_round_kinds(bool fin, int32_t kind, uint32_t nbusy) {
-  uint32_t run = 1u, waiting = 0u;
-#pragma unroll
-  for (int k = 1; k < kShadeKinds; ++k) {
-    const unsigned long long m = pt_ballot(fin && kind == k);
-    const uint32_t n = __builtin_popcount((uint32_t)m) + __builtin_popcount((uint32_t)(m >> 32));
-    if (n >= (uint32_t)PTMI_MK_SHADE_DEFER) run |= 1u << k;
-    else waiting += n;
-  }
-  if (nbusy == 0u || waiting >= (uint32_t)PTMI_MK_SHADE_DEFER_MAX) run = (1u << kShadeKinds) - 1u;
-  return run;
 }
 
 template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
@@ -354,7 +312,6 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   typename TravOf<TRAV>::T tr;
   tr.init(st);
   bool trav = false;  // a segment is in flight (traversal running or result pending)
-  bool deferred = false;  // traced, its shading left for a later round (PTMI_MK_SHADE_DEFER)
   bool need_seg = false;  // begin a segment after this pass's refill
   auto begin_segment = [&]() {
     const bool em = ps.mode == kModeMediumExit;
@@ -380,9 +337,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // 32-bit halves: a 64-bit popcount is compared with a VALU v_cmp_u64
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
-      // a round starts when a lane's segment has been traced since the last
-      // round (a deferred lane, PTMI_MK_SHADE_DEFER, waits for the next one)
-      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy() && !deferred) != 0ull) break;
+      if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -410,19 +365,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #if PTMI_MK_PRIO_TRAV >= 0
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
-#if PTMI_MK_SHADE_DEFER
-    bool shade_now;
-    {  // the kinds this round shades (deferred lanes are re-evaluated too)
-      const bool fin = trav && !tr.busy();
-      const int32_t kind = shade_kind(ps.mode == kModeMediumExit, tr);
-      const unsigned long long mb = pt_ballot(tr.busy());
-      const uint32_t run = shade_round_kinds(fin, kind, __builtin_popcount((uint32_t)mb) + __builtin_popcount((uint32_t)(mb >> 32)));
-      shade_now = fin && ((run >> kind) & 1u);
-      deferred = fin && !shade_now;
-    }
-#else
     const bool shade_now = trav && !tr.busy();
-#endif
     if (shade_now) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;

@@ -752,23 +752,29 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
 // Kernels of more than 16 stack slots stay at 4 (their 20+ KB LDS stacks allow no more).
 #define PTMI_WF_SCATTER_MIN_WAVES 5
 #endif
+// The medium waves' LDS stacks cap this kernel at 5 waves/SIMD. A/B on
+// MI355X (round 4): split into a medium launch (5 waves) and a launch for the
+// Perlin and surface lists without LDS stacks (5 / 6 waves), C3 -4 %
+// (profiles/r04/ab/ab_r04i_split_knobs_ruv.log).
+constexpr int32_t kScatterOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
+
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatter(DevScene sc, DevFrame fr, WfBufs wb,
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
-  constexpr int32_t kOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
   int32_t cnt[kLists][kShards], num[kLists], span[kLists];  // wave-uniform
   int32_t n = 0;
 #pragma unroll
   for (int l = 0; l < kLists; ++l) {
-    num[l] = list_counts(wb, par, kOrder[l], cnt[l]);
+    num[l] = list_counts(wb, par, kScatterOrder[l], cnt[l]);
     span[l] = (num[l] + 63) & ~63;
     n += span[l];
   }
   if (blockIdx.x < kShards && threadIdx.x < kLists)  // the next iteration's lists start empty
     *ctl_list(wb, par ^ 1, (int32_t)threadIdx.x, (int32_t)blockIdx.x) = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && counters && num[0] > 0) atomicAdd(counters + 1, (unsigned long long)num[0]);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && counters && num[0] > 0)
+    atomicAdd(counters + 1, (unsigned long long)num[0]);  // medium exit traversals
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0, ends[2] = {0u, 0u};
   for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
@@ -783,10 +789,14 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
     int32_t i = -1;
 #pragma unroll
     for (int k = 0; k < kLists; ++k)
-      if (l == k && j < num[k]) i = list_entry(wb, kOrder[k], cnt[k], j);
+      if (l == k && j < num[k]) i = list_entry(wb, kScatterOrder[k], cnt[k], j);
     if (i < 0) continue;  // the list's padding
-    if (l < 2) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, l == 1, n_ended, ends);
-    else shade_entry(sc, fr, wb, kOrder[l], i, n_ended, ends);  // kOrder[l] for l = 2, 3, 4: selects
+    int32_t lid = kScatterOrder[0];  // this wave's list (wave-uniform select, no indexed table)
+#pragma unroll
+    for (int k = 1; k < kLists; ++k)
+      if (l == k) lid = kScatterOrder[k];
+    if (lid == kListMedium || lid == kListNoise) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, lid == kListNoise, n_ended, ends);
+    else shade_entry(sc, fr, wb, lid, i, n_ended, ends);
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
 }
@@ -880,16 +890,13 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
   return e;
 }
 #ifndef PTMI_WF_RB_CHUNK
-#define PTMI_WF_RB_CHUNK 8
+#define PTMI_WF_RB_CHUNK 4  // A/B r04j: 4 +1.7 % C3, +1 % mesh fog over 8
 #endif
 #ifndef PTMI_WF_DRAIN_AT
 // A pipe whose read-back live count falls below capacity / PTMI_WF_DRAIN_AT
 // finishes its paths in one wf_drain launch (0 = never: one intersect and one
 // scatter launch per wave until the pipe is empty).
 #define PTMI_WF_DRAIN_AT 16
-#endif
-#ifndef PTMI_WF_DRAIN_JOINT
-#define PTMI_WF_DRAIN_JOINT 0
 #endif
 #ifndef PTMI_WF_CAPACITY_LOG2
 #define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
@@ -1002,26 +1009,11 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     if (err != hipSuccess) break;
     if (!waited) continue;  // first chunk: nothing read back yet
     bool any = false;
-    // PTMI_WF_DRAIN_JOINT: every pipe drains once all of them together are
-    // below the threshold (the pipes share the work pool, so they run dry
-    // together; a pipe whose own count lags would otherwise drain a chunk or
-    // two after the others and set the call's end)
-    bool drain_all = false;
-    if (PTMI_WF_DRAIN_JOINT && PTMI_WF_DRAIN_AT > 0) {
-      int64_t n_sum = 0, cap_sum = 0;
-      for (int p = 0; p < kPipes; ++p)
-        if (inflight[prev][p] && live[p]) {
-          n_sum += ps.pinned_live[prev * kPipes + p];
-          cap_sum += wbs[p].capacity;
-        }
-      drain_all = cap_sum > 0 && n_sum * PTMI_WF_DRAIN_AT < cap_sum;
-    }
     for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
       if (inflight[prev][p]) {
         const int32_t n_live = ps.pinned_live[prev * kPipes + p];
         live[p] = live[p] && n_live != 0;
-        if (live[p] && PTMI_WF_DRAIN_AT > 0 &&
-            (drain_all || (int64_t)n_live * PTMI_WF_DRAIN_AT < (int64_t)wbs[p].capacity)) {
+        if (live[p] && PTMI_WF_DRAIN_AT > 0 && (int64_t)n_live * PTMI_WF_DRAIN_AT < (int64_t)wbs[p].capacity) {
           // the pool is empty (some slot found no work) and few paths are left:
           // finish them in one launch, queued behind the iterations in flight
           const int pd = prof_begin(kProfWfDrain, st[p]);
