@@ -856,7 +856,114 @@ __device__ __forceinline__ float perlin_turb3(const DevScene& sc, pt_v3 p) {  //
   return fabsf(accum);
 }
 
-__device__ __forceinline__ pt_v3 eval_texture(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 hp) {
+// perlin_turb3 for the lanes of a wave that need it (need, at their p), the
+// whole wave working on two of them at a time: lane c of each half computes
+// term c of 24 — octave c >> 3, corner c & 7 — with perlin_noise's f32
+// expressions (the octave point p * 2^oc is perlin_turb3's repeated doubling,
+// exact), then every lane sums the two lanes' terms in perlin_noise's corner
+// order and perlin_turb3's octave order, the same operations in the same
+// sequence, so the result is bit-identical. A shading round with a few
+// Perlin-textured hits otherwise runs the whole 3-octave evaluation (six
+// dependent table loads, ~400 VALU) for one or two lanes; here a pair costs
+// two table round trips and ~150 VALU. Call from wave-uniform control flow.
+#ifndef PTMI_WAVE_TURB_NOINLINE
+// A call, not inlined: A/B on MI355X (round 4, parity-identical) against the
+// inlined form, C2 +1.4 %, C5 +1.3 %, C4 +1.2 % — inlined, its temporaries
+// raise the register pressure of the whole persistent loop (scratch 36 ->
+// 112 B/lane); as a call, the kernel keeps its 96 VGPRs and no scratch
+// (profiles/r04/ab/ab_r04m_wave_turb.log).
+#define PTMI_WAVE_TURB_NOINLINE 1
+#endif
+#if PTMI_WAVE_TURB_NOINLINE
+__device__ __attribute__((noinline)) float perlin_turb3_wave(const DevScene& sc, bool need, pt_v3 p, int lane) {
+#else
+__device__ __forceinline__ float perlin_turb3_wave(const DevScene& sc, bool need, pt_v3 p, int lane) {
+#endif
+  unsigned long long pend = pt_ballot(need);
+  float res = 0.0f;
+  const int c = lane & 31;
+  const int oc = c >> 3, di = (c >> 2) & 1, dj = (c >> 1) & 1, dk = c & 1;
+  const float oscale = oc == 0 ? 1.0f : (oc == 1 ? 2.0f : 4.0f);
+  const int32_t* px = sc.perlin_perm;
+  const int32_t* py = sc.perlin_perm + 256;
+  const int32_t* pz = sc.perlin_perm + 512;
+  while (pend != 0ull) {
+    const int l0 = (int)__builtin_ctzll(pend);
+    pend &= pend - 1ull;
+    const int l1 = pend != 0ull ? (int)__builtin_ctzll(pend) : l0;
+    if (pend != 0ull) pend &= pend - 1ull;
+    const bool hi = lane >= 32;
+    const float qx0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), l0));
+    const float qy0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), l0));
+    const float qz0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), l0));
+    const float qx1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), l1));
+    const float qy1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), l1));
+    const float qz1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), l1));
+    const pt_v3 tp = pt_scale(pt_v3f(hi ? qx1 : qx0, hi ? qy1 : qy0, hi ? qz1 : qz0), oscale);
+    const float fx = floorf(tp.x), fy = floorf(tp.y), fz = floorf(tp.z);
+    const float u = tp.x - fx, v = tp.y - fy, w = tp.z - fz;
+    const int32_t i = pt_f2i(fx), j = pt_f2i(fy), k = pt_f2i(fz);
+    const float uu = u * u * (3.0f - 2.0f * u);
+    const float vv = v * v * (3.0f - 2.0f * v);
+    const float ww = w * w * (3.0f - 2.0f * w);
+    const int32_t idx = px[(i + di) & 255] ^ py[(j + dj) & 255] ^ pz[(k + dk) & 255];
+    const float4 g = sc.perlin_vec[idx];
+    const pt_v3 wt = pt_v3f(u - (float)di, v - (float)dj, w - (float)dk);
+    const float fxw = di ? uu : (1.0f - uu);
+    const float fyw = dj ? vv : (1.0f - vv);
+    const float fzw = dk ? ww : (1.0f - ww);
+    const float term = fxw * fyw * fzw * pt_dot(pt_v3f(g.x, g.y, g.z), wt);
+    // corner sums as a left fold along each 8-lane octave group: after step
+    // s, lane c holds (((0 + t[c-s]) + t[c-s+1]) ... + t[c]) (DPP row_shr:1
+    // moves lane c-1's partial to lane c; groups do not cross 16-lane rows),
+    // so lane 8 * oc + 7 ends with perlin_noise's accumulation
+    float acc = 0.0f + term;
+#pragma unroll
+    for (int q = 1; q < 8; ++q)
+      acc = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc), 0x111, 0xf, 0xf, false)) + term;
+    const int ai = __float_as_int(acc);
+    float t0 = 0.0f, t1 = 0.0f, wgt = 1.0f;
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      t0 += wgt * __int_as_float(__builtin_amdgcn_readlane(ai, 8 * o + 7));
+      t1 += wgt * __int_as_float(__builtin_amdgcn_readlane(ai, 32 + 8 * o + 7));
+      wgt *= 0.5f;
+    }
+    if (lane == l0) res = fabsf(t0);
+    if (lane == l1) res = fabsf(t1);
+  }
+  return res;
+}
+
+// image_texture (kernels.py:976-1008; get_sphere_uv :79-102): the Earth-map
+// lookup of a sphere hit (magenta for other primitives).
+// (A/B, not kept: as a call, not inlined, the megakernel spills 416 B/lane:
+// a call from the divergent shading code saves the whole live state.)
+__device__ __forceinline__ pt_v3 image_texture(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 hp) {
+  if (leaf_type(ref) != kSphere) return pt_v3f(1.0f, 0.0f, 1.0f);
+  int32_t img = m.image();
+  float4 s = sc.spheres[leaf_index(ref)];
+  pt_v3 n = pt_normalize(pt_sub(hp, pt_v3f(s.x, s.y, s.z)));  // get_sphere_uv, kernels.py:79-102
+  float phi = pt_acosf(-n.y);
+  float theta = pt_atan2f(-n.z, n.x) + PT_PI_F;
+  float u = theta / PT_2PI_F;
+  float v = phi / PT_PI_F;
+  if (img < 0 || img >= sc.num_images) return pt_v3f(1.0f, 1.0f, 1.0f);
+  int32_t W = sc.img_w[img], H = sc.img_h[img];
+  u = pt_maxf(0.0f, pt_minf(1.0f, u));
+  v = 1.0f - pt_maxf(0.0f, pt_minf(1.0f, v));
+  int32_t ii = pt_f2i(u * (float)W);
+  int32_t jj = pt_f2i(v * (float)H);
+  ii = ii < 0 ? 0 : (ii > W - 1 ? W - 1 : ii);
+  jj = jj < 0 ? 0 : (jj > H - 1 ? H - 1 : jj);
+  uint32_t px = sc.texels[sc.img_offset[img] + jj * W + ii];
+  return pt_v3f((float)(px & 0xffu) / 255.0f, (float)((px >> 8) & 0xffu) / 255.0f,
+                (float)((px >> 16) & 0xffu) / 255.0f);
+}
+
+// has_turb: turb is perlin_turb3(sc, hp), already evaluated (perlin_turb3_wave)
+__device__ __forceinline__ pt_v3 eval_texture(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 hp,
+                                             bool has_turb = false, float turb = 0.0f) {
   // kernels.py:925-1017
   int32_t tex = m.tex_type();
   pt_v3 c1 = pt_v3f(m.m2.x, m.m2.y, m.m2.z);
@@ -870,29 +977,9 @@ __device__ __forceinline__ pt_v3 eval_texture(const DevScene& sc, int32_t ref, c
     int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
     return (s % 2 == 0) ? c1 : pt_v3f(m.m3.x, m.m3.y, m.m3.z);
   }
-  if (tex == 2) {
-    if (leaf_type(ref) != kSphere) return pt_v3f(1.0f, 0.0f, 1.0f);
-    int32_t img = m.image();
-    float4 s = sc.spheres[leaf_index(ref)];
-    pt_v3 n = pt_normalize(pt_sub(hp, pt_v3f(s.x, s.y, s.z)));  // get_sphere_uv, kernels.py:79-102
-    float phi = pt_acosf(-n.y);
-    float theta = pt_atan2f(-n.z, n.x) + PT_PI_F;
-    float u = theta / PT_2PI_F;
-    float v = phi / PT_PI_F;
-    if (img < 0 || img >= sc.num_images) return pt_v3f(1.0f, 1.0f, 1.0f);
-    int32_t W = sc.img_w[img], H = sc.img_h[img];
-    u = pt_maxf(0.0f, pt_minf(1.0f, u));
-    v = 1.0f - pt_maxf(0.0f, pt_minf(1.0f, v));
-    int32_t ii = pt_f2i(u * (float)W);
-    int32_t jj = pt_f2i(v * (float)H);
-    ii = ii < 0 ? 0 : (ii > W - 1 ? W - 1 : ii);
-    jj = jj < 0 ? 0 : (jj > H - 1 ? H - 1 : jj);
-    uint32_t px = sc.texels[sc.img_offset[img] + jj * W + ii];
-    return pt_v3f((float)(px & 0xffu) / 255.0f, (float)((px >> 8) & 0xffu) / 255.0f,
-                  (float)((px >> 16) & 0xffu) / 255.0f);
-  }
+  if (tex == 2) return image_texture(sc, ref, m, hp);
   if (tex == 3) {
-    float nv = pt_sinf(scale * hp.z + 10.0f * perlin_turb3(sc, hp));
+    float nv = pt_sinf(scale * hp.z + 10.0f * (has_turb ? turb : perlin_turb3(sc, hp)));
     return pt_scale(pt_scale(c1, 0.5f), 1.0f + nv);
   }
   return pt_v3f(1.0f, 1.0f, 1.0f);
@@ -974,12 +1061,12 @@ enum : int32_t { kRuvNone = 0, kRuvMetal = 1, kRuvIso = 2, kRuvMedium = 3 };
 
 __device__ __forceinline__ int32_t scatter_begin(const DevScene& sc, int32_t ref, const Mat& m, pt_v3 dir,
                                                  pt_v3 hp, pt_v3 n, Rng& r, pt_v3& sdir, pt_v3& att,
-                                                 bool& scattered) {
+                                                 bool& scattered, bool has_turb = false, float turb = 0.0f) {
   int32_t mt = m.mat_type();
   sdir = pt_v3f(0.0f, 0.0f, 0.0f);
   att = pt_v3f(1.0f, 1.0f, 1.0f);
   scattered = false;
-  if (mt == 0 || mt == 4) att = eval_texture(sc, ref, m, hp);  // one texture site (draws nothing)
+  if (mt == 0 || mt == 4) att = eval_texture(sc, ref, m, hp, has_turb, turb);  // one texture site (draws nothing)
   if (mt == 0) {
     sdir = random_cosine_direction(n, r);
     scattered = true;

@@ -110,6 +110,13 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // round 2 measured C2 -1.1 % with the code of the time).
 #define PTMI_MK_ONE_RUV 1
 #endif
+#ifndef PTMI_MK_WAVE_TURB
+// Turbulence of a shading round's Perlin-textured hits by the whole wave
+// (perlin_turb3_wave, pt_device.hpp). Ablation on MI355X (round 4, textures
+// replaced by constants, not parity): without the Perlin evaluation C2 +5 %,
+// C5 +4.8 %; without the image lookup +1.2 % (profiles/r04/ab/ab_r04l_texture_ablation.log).
+#define PTMI_MK_WAVE_TURB 1
+#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
@@ -366,6 +373,16 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
     const bool shade_now = trav && !tr.busy();
+#if PTMI_MK_WAVE_TURB
+    // Perlin-textured surface hits of this round: their turbulence by the
+    // whole wave (perlin_turb3_wave), before the divergent shading below
+    const bool pn = shade_now && ps.mode != kModeMediumExit && tr.any() && leaf_class(tr.best) == PTMI_CLASS_NOISE;
+    float pturb = 0.0f;
+    if (pt_ballot(pn) != 0ull) pturb = perlin_turb3_wave(sc, pn, pt_add(ps.o, pt_scale(ps.dir, tr.closest)), lane);
+#else
+    constexpr bool pn = false;
+    constexpr float pturb = 0.0f;
+#endif
     if (shade_now) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
@@ -430,7 +447,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           n = hit_normal(sc, sref, hp, ps.dir);
           ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
 #if PTMI_MK_ONE_RUV
-          ruv = scatter_begin(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att, scattered);
+          ruv = scatter_begin(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att, scattered, pn && !exit_mode, pturb);
 #else
           scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
 #endif
