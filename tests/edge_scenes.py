@@ -17,13 +17,21 @@
   N - 1 > 62). The flattened arrays follow the reference's layout
   (sah_bvh_builder.py:338-418 flatten: preorder, left child at i + 1, node
   box = union of the children's boxes, internal prim_type/prim_idx = -1).
+* ``marble``: noise-textured Lambertian spheres at four scales over a
+  noise-textured ground, with a solid Lambertian, a metal sphere and a
+  light: most shading rounds of the megakernel hold several Perlin hits, so
+  the wave-cooperative turbulence (perlin_turb3_wave) runs several passes,
+  with odd and even counts.
 """
 from __future__ import annotations
+
+import random
 
 import numpy as np
 
 from ptmi import scene_data as sd
-from ptmi.core import Sphere, camera, color, hittable_list, lambertian, metal, point3, vec3
+from ptmi.core import (Sphere, camera, color, diffuse_light, hittable_list, lambertian, metal, noise_texture,
+                       point3, vec3)
 from ptmi.scenes import _wrap
 
 BG = (0.6, 0.7, 0.9)
@@ -116,6 +124,16 @@ def edge_scene(name, width=96):
             order = np.concatenate([np.flatnonzero(small)[np.argsort(sa.sphere_data[small, 0], kind='stable')],
                                     np.flatnonzero(~small)])
         sa.bvh = _linear_bvh(sa, order)
+    elif name == 'marble':
+        random.seed(7)
+        w = hittable_list()
+        w.add(Sphere.stationary(point3(0, -100.4, 0), 100.0, lambertian.from_texture(noise_texture(4.0))))
+        for k, (x, scale) in enumerate([(-2.4, 1.0), (-0.8, 3.0), (0.8, 6.0), (2.4, 12.0)]):
+            w.add(Sphere.stationary(point3(x, 0.5, -0.3 * k), 0.75, lambertian.from_texture(noise_texture(scale))))
+        w.add(Sphere.stationary(point3(0.0, 1.9, -1.0), 0.6, lambertian.from_color(color(0.7, 0.6, 0.2))))
+        w.add(Sphere.stationary(point3(-1.5, 1.6, 0.8), 0.4, metal(color(0.8, 0.8, 0.8), 0.2)))
+        w.add(Sphere.stationary(point3(1.6, 1.7, 0.5), 0.35, diffuse_light.from_color(color(4.0, 4.0, 4.0))))
+        sa = sd.compile_world(_wrap(w.objects))
     else:
         raise KeyError(name)
     _cache[key] = (sa, _camera(width, along_x=name.startswith('chainx')), BG)

@@ -9,7 +9,9 @@ C-ABI, against the CPU oracle, same bar as test_gpu_parity: per-pixel L-inf
   stack, so pushes are dropped (kernels.py:719-740): the reference-stack walk;
 * max_depth 1 and 2 (kernels.py:1139-1141 / 1383, SURVEY Q13/Q14);
 * a zero-sample call, which must leave the accumulator untouched;
-* 1x1, 3x1 and 13x7 frames (smaller than a wave or the pipes' work, ragged 8x8 squares).
+* 1x1, 3x1 and 13x7 frames (smaller than a wave or the pipes' work, ragged 8x8 squares);
+* a scene of noise-textured surfaces, so the megakernel's shading rounds
+  evaluate the turbulence of many lanes at once.
 """
 import numpy as np
 import pytest
@@ -66,6 +68,12 @@ def test_empty_scene_is_background(variant):
 def test_single_primitive_root_leaf(variant):
     got = _check('single', variant, 4)
     assert not np.allclose(got, got[0, 0])  # the sphere is in view
+
+
+@pytest.mark.parametrize('variant', ['mk', 'wf'])
+def test_noise_textured_scene(variant):
+    """perlin_turb3_wave: 2..64 Perlin lanes per shading round, bit-identical to the oracle."""
+    _check('marble', variant, 4)
 
 
 @pytest.mark.parametrize('name', ['chain22', 'chain29', 'chain52'])
