@@ -114,6 +114,87 @@ __device__ __forceinline__ pt_v3 random_unit_vector(Rng& r) {  // kernels.py:29-
   }
 }
 
+// random_unit_vector for the lanes of a wave that need one (need; call from
+// wave-uniform code), the other lanes testing their candidates: the
+// rejection loop's candidates are independent counter-based draws (candidate
+// j of a lane at counter n is the three draws n + 3j, n + 3j + 1, n + 3j + 2),
+// so with k lanes pending each gets C = 64 / k (at most 16) lanes, lane j of
+// its group tests candidate j, and the lane takes its first accepted one and
+// advances its counter past it: the same draws, the same first accepted
+// candidate and the same normalisation as its own loop, bit-identical. An
+// ablation with the loop replaced by one candidate (not parity) put the loop
+// at 2.3 % of C2 and 4.9 % of C4 (profiles/r04/ab/ab_r04q_ruv_ablation.log): it
+// runs to the wave's unluckiest lane (acceptance pi/6 per candidate). More
+// than 32 lanes pending: each lane runs its own loop. A/B on MI355X (round 4,
+// parity-identical) against the divergent site: C4 +1.4 %, C2 +0.2 %, C5
+// +0.1 % (the split of the shading code around the uniform site alone: C4
+// -1.3 %; profiles/r04/ab/ab_r04r_wave_ruv.log).
+#ifndef PTMI_RUV_WAVE_NOINLINE
+#define PTMI_RUV_WAVE_NOINLINE 0  // inlined: A/B within noise of the call (C4 +1.4 vs +1.3 %, C5 +0.1 vs -0.2 %)
+#endif
+struct RuvOut {
+  pt_v3 v;
+  uint32_t n;  // the lane's counter after its draws
+};
+#if PTMI_RUV_WAVE_NOINLINE
+__device__ __attribute__((noinline)) RuvOut random_unit_vector_wave(uint32_t key, uint32_t ctr, bool need, int lane) {
+#else
+__device__ __forceinline__ RuvOut random_unit_vector_wave(uint32_t key, uint32_t ctr, bool need, int lane) {
+#endif
+  unsigned long long pend = __builtin_amdgcn_ballot_w64(need);
+  const uint32_t k0 = (uint32_t)__popcll(pend);
+  if (k0 > 32u) {  // too many for a group each: the plain loop
+    Rng r{key, ctr};
+    pt_v3 v = pt_v3f(0.0f, 0.0f, 0.0f);
+    if (need) v = random_unit_vector(r);
+    return RuvOut{v, r.n};
+  }
+  pt_v3 p = pt_v3f(0.0f, 0.0f, 0.0f);
+  uint32_t n0 = ctr;
+  while (pend != 0ull) {
+    const uint32_t k = (uint32_t)__popcll(pend);
+    const uint32_t lg = k <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(k - 1u);  // ceil(log2 k)
+    const uint32_t lc = lg >= 2u ? 6u - lg : 4u;                                 // log2 C, C <= 16
+    const bool pending = (pend >> lane) & 1ull;
+    const uint32_t lo = (uint32_t)pend, hi = (uint32_t)(pend >> 32);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+    const uint32_t nrank = __builtin_amdgcn_mbcnt_hi(~hi, __builtin_amdgcn_mbcnt_lo(~lo, 0u));
+    // a permutation of the lanes: pending lanes to [0, k) in lane order, the rest after
+    const int dst = (int)(pending ? rank : k + nrank);
+    const int owner_of = __builtin_amdgcn_ds_permute(dst << 2, lane);  // lane r < k: the r-th pending lane
+    const int g = lane >> lc, j = lane & ((1 << lc) - 1);
+    const bool valid = (uint32_t)g < k;
+    const int owner = __builtin_amdgcn_ds_bpermute((valid ? g : 0) << 2, owner_of);
+    const uint32_t okey = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)key);
+    const uint32_t on = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)n0) + 3u * (uint32_t)j;
+    const float x = pt_rand(okey, on) * 2.0f - 1.0f;
+    const float y = pt_rand(okey, on + 1u) * 2.0f - 1.0f;
+    const float z = pt_rand(okey, on + 2u) * 2.0f - 1.0f;
+    const float l2 = pt_dot(pt_v3f(x, y, z), pt_v3f(x, y, z));
+    const unsigned long long acc = __builtin_amdgcn_ballot_w64(valid && l2 < 1.0f && l2 > 1e-20f);
+    // a pending lane: its group's first accepted candidate, if any
+    const uint32_t base = pending ? rank << lc : 0u;  // < 64: k groups of C lanes
+    const unsigned long long gbits = (acc >> base) & ((1ull << (1u << lc)) - 1ull);
+    const uint32_t jf = gbits != 0ull ? (uint32_t)__builtin_ctzll(gbits) : 0u;
+    const int src = (int)(base + jf);
+    const float ax = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(x)));
+    const float ay = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(y)));
+    const float az = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(z)));
+    bool still = false;
+    if (pending) {
+      if (gbits != 0ull) {
+        p = pt_v3f(ax, ay, az);
+        n0 += 3u * (jf + 1u);
+      } else {
+        n0 += 3u << lc;
+        still = true;
+      }
+    }
+    pend = __builtin_amdgcn_ballot_w64(still);
+  }
+  return RuvOut{need ? pt_normalize(p) : p, n0};
+}
+
 __device__ __forceinline__ pt_v3 random_cosine_direction(pt_v3 n, Rng& r) {  // kernels.py:42-71
   float r1 = r.next();
   float r2 = r.next();

@@ -101,14 +101,16 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // whose segment needs an expensive kind of shading waits until 4 / 8 / 12 /
 // 16 lanes need the same kind): C2 -0.5 %, C4 -1 %
 // (profiles/r04/ab/ab_r04i_split_knobs_ruv.log, ab_wf_layout_drain_mk_shade_defer.log).
-#ifndef PTMI_MK_ONE_RUV
 // One random_unit_vector call site per shading round (scatter_begin /
 // scatter_end, pt_device.hpp) for the medium scatter, metal fuzz and
 // isotropic, instead of three divergent copies of the rejection loop: the
 // loop then runs once, to the wave's longest lane. A/B on MI355X (round 4,
 // parity-identical): C4 +2.1 %, C2 +-0.3 % (profiles/r04/ab/ab_r04i_split_knobs_ruv.log;
 // round 2 measured C2 -1.1 % with the code of the time).
-#define PTMI_MK_ONE_RUV 1
+#ifndef PTMI_MK_WAVE_RUV
+// ... and that site in wave-uniform code, the wave sharing the loop
+// (random_unit_vector_wave, pt_device.hpp).
+#define PTMI_MK_WAVE_RUV 1
 #endif
 #ifndef PTMI_MK_WAVE_TURB
 // Turbulence of a shading round's Perlin-textured hits by the whole wave
@@ -383,15 +385,19 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     constexpr bool pn = false;
     constexpr float pturb = 0.0f;
 #endif
+    // Shading, in two halves around the round's one random_unit_vector site
+    // (medium scatter, metal fuzz, isotropic), which runs in wave-uniform code
+    // so that the wave can share its rejection loop (random_unit_vector_wave).
+    bool done = false, scattered = false, passthrough = false, to_medium = false;
+    pt_v3 hp = pt_v3f(0.0f, 0.0f, 0.0f), sdir = hp, att = hp, n = hp;
+    int32_t ruv = kRuvNone, sref = 0;
+    float4 m0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the metal's albedo and fuzz (scatter_end)
     if (shade_now) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
       const bool hit = tr.any();
       const float t = tr.closest;
       const int32_t ref = tr.best;
-
-      bool done = false, scattered = false, passthrough = false, to_medium = false;
-      pt_v3 hp, sdir, att;
       int32_t g = -1;
       if (!exit_mode) {
         if (!hit) {
@@ -412,11 +418,8 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       if (g >= 0 && !to_medium) {
         const Mat m = load_mat(sc, g);
         bool surface = !exit_mode;
-        int32_t sref = ref;
+        sref = ref;
         float st = t;
-        pt_v3 n = pt_v3f(0.0f, 0.0f, 0.0f);
-        int32_t ruv = kRuvNone;
-        (void)ruv;
         if (exit_mode) {
           ps.mode = kModeTrace;
           float t_exit;
@@ -424,11 +427,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           // apply_constant_medium, kernels.py:421-448 (density m3.w)
           if (medium_step(hit, t, ps.t_entry, m.m3.w, ps.o, ps.dir, ps.rng, mp, t_exit)) {
             hp = mp;  // kernels.py:1082-1097
-#if PTMI_MK_ONE_RUV
             ruv = kRuvMedium;
-#else
-            sdir = random_unit_vector(ps.rng);
-#endif
             att = pt_v3f(m.m4.x, m.m4.y, m.m4.z);
             scattered = true;
           } else if (t_exit > 0.0f) {  // kernels.py:1100-1110
@@ -446,21 +445,37 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           hp = pt_add(ps.o, pt_scale(ps.dir, st));
           n = hit_normal(sc, sref, hp, ps.dir);
           ps.color = pt_add(ps.color, pt_mul(ps.thr, emitted(m)));  // kernels.py:1123-1124
-#if PTMI_MK_ONE_RUV
           ruv = scatter_begin(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att, scattered, pn && !exit_mode, pturb);
-#else
-          scattered = scatter(sc, sref, m, ps.dir, hp, n, ps.rng, sdir, att);
-#endif
+          m0 = m.m0;
         }
-#if PTMI_MK_ONE_RUV
-        if (ruv != kRuvNone) {  // one random_unit_vector site: medium, metal fuzz, isotropic
-          const pt_v3 v = random_unit_vector(ps.rng);
-          if (ruv == kRuvMedium) sdir = v;
-          else scattered = scatter_end(sc, ruv, sref, m, hp, n, v, sdir, att);
-        }
-#endif
       }
-
+    }
+    // one random_unit_vector site per round: medium, metal fuzz, isotropic
+#if PTMI_MK_WAVE_RUV
+    if (pt_ballot(ruv != kRuvNone) != 0ull) {
+      const RuvOut ro = random_unit_vector_wave(ps.rng.key, ps.rng.n, ruv != kRuvNone, lane);
+      ps.rng.n = ro.n;
+      if (ruv == kRuvMedium) {
+        sdir = ro.v;
+      } else if (ruv != kRuvNone) {
+        Mat mm{};
+        mm.m0 = m0;
+        scattered = scatter_end(sc, ruv, sref, mm, hp, n, ro.v, sdir, att);
+      }
+    }
+#else
+    if (ruv != kRuvNone) {
+      const pt_v3 v = random_unit_vector(ps.rng);
+      if (ruv == kRuvMedium) {
+        sdir = v;
+      } else {
+        Mat mm{};
+        mm.m0 = m0;
+        scattered = scatter_end(sc, ruv, sref, mm, hp, n, v, sdir, att);
+      }
+    }
+#endif
+    if (shade_now) {
       if (!done && !to_medium) {
         if (scattered) {  // kernels.py:1131-1157
           ps.o = hp;
