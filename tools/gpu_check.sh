@@ -15,6 +15,7 @@
 #   parity_variants  the GPU parity tests against each variants/*.so
 #   cache_mk / cache_wf   L1/L2 hit-rate PMC pass of one 32-spp call (tools/pmc_cache_summary.py reads it)
 #   lat_mk / lat_wf       VALU / wait PMC passes (tools/gpu_pmc_latency.sh; tools/pmc_valu.py reads them)
+#   ta_mk / ta_wf         texture-address (vector memory address) unit busy cycles of one 32-spp call
 #   abtrace_<lib>_<mk|wf> rocprofv3 kernel trace + stats of tools/ab.py (64 spp x 2) with variants/libptmi_<lib>.so
 #                         (<lib> = default: the default build)
 #   abpmc_<lib>_<mk|wf>   FETCH_SIZE, WRITE_SIZE and cache-hit PMC passes of tools/ab.py (32 spp x 1), same libs
@@ -51,6 +52,7 @@ for s in $STEPS; do
     parity_variants) for lib in path-tracer-python_amd/ptmi/_lib/variants/*.so; do
         step parity_$(basename $lib .so) 600 env PTMI_LIB=$PWD/$lib python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edge.py -x -q --timeout 300 --timeout-method thread; done ;;
     cache_mk|cache_wf) v=${s#cache_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_cache" -o $v -- python tools/ab.py $v 32 1 ;;
+    ta_mk|ta_wf) v=${s#ta_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_ta" -o $v -- python tools/ab.py $v 32 1 ;;
     lat_mk|lat_wf) v=${s#lat_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_$v bash tools/gpu_pmc_latency.sh ;;
     probe) step probe 600 bash tools/gpu_probe.sh ;;
     abtrace_*) r=${s#abtrace_}; name=${r%_*}; mode=${r##*_}
