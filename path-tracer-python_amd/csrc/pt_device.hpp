@@ -482,6 +482,9 @@ __device__ unsigned long long g_probe[16];
 #endif
 
 constexpr uint32_t kNodeBytes = 80;
+#ifndef PTMI_NODE_CENTRE_LOAD
+#define PTMI_NODE_CENTRE_LOAD 0
+#endif
 
 // In-flight traversal of one ray: begin (root test, push root) and one pop
 // of the loop per step, so a kernel can interleave steps of different rays'
@@ -622,8 +625,17 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
   const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
   // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
+#if PTMI_NODE_CENTRE_LOAD
   const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
   const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
+#else
+  // x / y centres from the boxes just loaded, (min + max) * 0.5 as the host
+  // packs them (bit-identical): four 16-B loads per node instead of five. A/B
+  // on MI355X (round 4, parity-identical): C3 +2.4 %, C2 +0.9 %, C5 +0.9 %, C4
+  // +-0 (profiles/r04/ab/ab_r04x_node_centres.log; the megakernel's
+  // texture-address unit is 70 % busy, profiles/r04/pmc_ta/).
+  const pt_f2 cx = (lox + hix) * pt_f2s(0.5f), cy = (loy + hiy) * pt_f2s(0.5f), cz = {R.z, R.w};
+#endif
   const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
   const bool ln = dist.x < dist.y;  // child 0 is the near one; the far child is pushed first
   const bool h0 = X0 >= E0, h1 = X1 >= E1;
