@@ -42,7 +42,9 @@ enum {
  *             children form packed-f32 pairs: {min.x c0,c1, min.y c0,c1 |
  *             min.z c0,c1, max.x c0,c1 | max.y c0,c1, max.z c0,c1 |
  *             ref0, ref1 (i32 bits), centre.z c0,c1 | centre.x c0,c1,
- *             centre.y c0,c1}; centre = (min + max) * 0.5f in f32.
+ *             centre.y c0,c1}; centre = (min + max) * 0.5f in f32 (the
+ *             kernels read the first 64 B and compute centre.x / .y from
+ *             the boxes, the same operations; the last 16 B stay packed).
  *             ref >= 0: internal node, as its BYTE offset in nodes
  *             (index x 80: the traversal adds it to the node base with
  *             no index scaling); ref < 0: leaf code

@@ -481,10 +481,12 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 __device__ unsigned long long g_probe[16];
 #endif
 
+// Node stride (include/ptmi.h, ptmi_node_bytes()). The traversal reads the
+// first 64 B (boxes, refs, z centres) and computes the x / y centres; the
+// last 16 B hold them precomputed and are not read. A/B on MI355X (round 4,
+// parity-identical): a 64-B stride without them, C2 -1.2 %, C4 -1.1 %, C5
+// -0.7 %, C3 +-0 (profiles/r04/ab/ab_r04z_node64.log), so the stride stays 80.
 constexpr uint32_t kNodeBytes = 80;
-#ifndef PTMI_NODE_CENTRE_LOAD
-#define PTMI_NODE_CENTRE_LOAD 0
-#endif
 
 // In-flight traversal of one ray: begin (root test, push root) and one pop
 // of the loop per step, so a kernel can interleave steps of different rays'
@@ -613,7 +615,7 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
   const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
   const float tmin = tr.tmin;
-  gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // 80-B node at byte offset ref
+  gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // the node at byte offset ref
   const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
   const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
   const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
@@ -625,17 +627,15 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
   const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
   // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
-#if PTMI_NODE_CENTRE_LOAD
-  const pt_f4 Cxy = nd[4];  // precomputed (min + max) * 0.5, identical rounding
-  const pt_f2 cx = {Cxy.x, Cxy.y}, cy = {Cxy.z, Cxy.w}, cz = {R.z, R.w};
-#else
-  // x / y centres from the boxes just loaded, (min + max) * 0.5 as the host
-  // packs them (bit-identical): four 16-B loads per node instead of five. A/B
-  // on MI355X (round 4, parity-identical): C3 +2.4 %, C2 +0.9 %, C5 +0.9 %, C4
+  // x / y centres from the boxes just loaded, (min + max) * 0.5 as the
+  // reference computes them (bit-identical); the z centres come with the
+  // refs. A/B on MI355X (round 4, parity-identical), against loading all
+  // three (a fifth 16-B load per node): C3 +2.4 %, C2 +0.9 %, C5 +0.9 %, C4
   // +-0 (profiles/r04/ab/ab_r04x_node_centres.log; the megakernel's
-  // texture-address unit is 70 % busy, profiles/r04/pmc_ta/).
+  // texture-address unit is 70 % busy, profiles/r04/pmc_ta/); the refs alone
+  // as an 8-B load with the z centres computed too: C2 -4 %, C3 -2 %
+  // (ab_r04y_node_refs_only.log).
   const pt_f2 cx = (lox + hix) * pt_f2s(0.5f), cy = (loy + hiy) * pt_f2s(0.5f), cz = {R.z, R.w};
-#endif
   const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
   const bool ln = dist.x < dist.y;  // child 0 is the near one; the far child is pushed first
   const bool h0 = X0 >= E0, h1 = X1 >= E1;
