@@ -65,7 +65,7 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #endif
 
 #ifndef PTMI_MK_STEP_UNROLL
-#define PTMI_MK_STEP_UNROLL 3  // A/B with SHADE_AT 16: 3 pops per header pass +1.9 % C2, +2.6 % C4 (2: +1.5 %, 4: +1.6 %)
+#define PTMI_MK_STEP_UNROLL 4  // A/B: 3 pops per header pass +1.9 % C2, +2.6 % C4 over 1 (round 1; 2: +1.5 %, 4: +1.6 %); round 4, with the 4-load node visits: 4 over 3 C2 +0.8 %, C5 +0.5 %, C4 +0.2 % (profiles/r04/ab/ab_r04su_step_unroll.log)
 #endif
 
 #ifndef PTMI_MK_PRIO_TRAV
