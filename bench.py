@@ -99,9 +99,11 @@ def parse(argv=None):
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--save-image', default='')
-    p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default='nccl',
-                   help='nccl = RCCL over xGMI (the product path); gloo only to rehearse the multi-rank flow '
-                        'with several ranks on one GPU (host-side collective)')
+    p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default=None,
+                   help='nccl = RCCL over xGMI (the product path, the default for --gpus > 1); gloo only to '
+                        'rehearse the multi-rank flow with several ranks on one GPU (host-side collective). '
+                        'Given explicitly with --gpus 1, the process group is created at world size 1 and '
+                        'every collective of the N-GPU flow runs (gather, all-reduce MAX, all-gather)'),
     p.add_argument('--no-overlap', action='store_true',
                    help='megakernel: each step waits for the previous one to finish (default: consecutive '
                         'steps overlap, Integrator.render_mk_overlapped)')
@@ -118,6 +120,8 @@ def parse(argv=None):
     a.variant = a.variant or variant
     a.spp_per_step = a.spp_per_step or sps
     a.steps = a.steps or steps
+    a.process_group = a.gpus > 1 or a.dist_backend is not None
+    a.dist_backend = a.dist_backend or 'nccl'
     return a
 
 
@@ -290,16 +294,18 @@ def throughput(samples_all, elapsed_max_s):
     return samples_all / elapsed_max_s / 1e6
 
 
-def gather_ranks(vals, dev, world):
-    """Per-rank float rows (all_gather) -> list of lists; [vals] for world 1."""
-    if world == 1:
-        return [list(vals)]
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor(vals, dtype=torch.float64, device=dev)
-    out = [torch.zeros_like(t) for _ in range(world)]
-    dist.all_gather(out, t)
-    return [o.cpu().tolist() for o in out]
+def gather_ranks(vals, dev, world=None):
+    """Per-rank float rows (one all_gather, ptmi.distributed.gather_ranks) ->
+    list of lists; [vals] without a process group."""
+    from ptmi.distributed import gather_ranks as _gather
+    return _gather(vals, dev)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
 
 
 def main():
@@ -315,8 +321,11 @@ def main():
     # one process per GPU; the gloo rehearsal may put several ranks on one device
     dev_index = local_rank if a.dist_backend == 'nccl' else local_rank % max(1, torch.cuda.device_count())
     dev = torch.device('cuda', dev_index)
-    if world > 1:
+    pg = a.process_group  # --gpus > 1, or an explicit --dist-backend at --gpus 1
+    if pg:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if 'RANK' not in os.environ:  # a plain `python bench.py --gpus 1 --dist-backend nccl`
+            os.environ.update(RANK='0', WORLD_SIZE='1', MASTER_PORT=os.environ.get('MASTER_PORT', str(_free_port())))
         torch.cuda.set_device(dev)
         if a.dist_backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
@@ -324,7 +333,7 @@ def main():
             dist.init_process_group('gloo')
         if dist.get_world_size() != world:
             sys.exit(f'--gpus {world} but torch.distributed has {dist.get_world_size()} ranks')
-    world_size = dist.get_world_size() if world > 1 else 1
+    world_size = dist.get_world_size() if pg else 1
 
     run = BenchRun(a, dev, rank, world)
     integ, frame, sa, cam, bg = run.integ, run.frame, run.sa, run.cam, run.bg
@@ -342,7 +351,7 @@ def main():
     acc.zero_()  # all rows: the warm-up gather left other ranks' bands on the root
     integ.reset_counters()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
 
     # Per-kernel durations (roofline): HIP events around every launch, on the
@@ -354,18 +363,18 @@ def main():
     inline = a.variant == 'mk'
     with _lib.KernelTimer(max_launches=100_000 if inline else 0) as kt:
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         t0 = time.perf_counter()
         for k in range(a.steps):
             run.step(acc, a.warmup + k)
         t_render_end = None
-        if world > 1:
+        if pg:
             torch.cuda.synchronize(dev)  # this rank's own render time (per-rank balance), then the gather
             t_render_end = time.perf_counter()
         assemble_image(acc, shard, dst=0)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         elapsed_rank = time.perf_counter() - t0
     render_rank = (t_render_end - t0) if t_render_end is not None else elapsed_rank
@@ -395,9 +404,12 @@ def main():
     unit_name, unit_bytes = ALGO_BYTES[dom]
     if unit_bytes is None:
         unit_bytes = b_sample
-    units = {'wf_intersect': cnt['segments'], 'wf_scatter': cnt['segments'],
+    # segments traced by the wavefront's tail launch (wf_drain) belong to its
+    # time, not to wf_intersect's / wf_scatter's
+    tail = (integ.tail_segments() or 0) if a.variant == 'wf' else 0
+    units = {'wf_intersect': cnt['segments'] - tail, 'wf_scatter': cnt['segments'] - tail,
              'megakernel': samples_rank,
-             'wf_generate': 0, 'wf_drain': 0, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
+             'wf_generate': 0, 'wf_drain': tail, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
              'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]
     dom_ms = prof[dom]['busy_ms']
     launches = prof[dom]['launches']
@@ -454,6 +466,10 @@ def main():
         'kernels_ms': {k: round(v['ms'], 3) for k, v in prof.items() if v['launches']},
         'kernels_busy_ms': {k: round(v['busy_ms'], 3) for k, v in prof.items() if v['launches']},
         'segments_per_sample': round(S, 4),
+        'tail_segments_per_sample': round(tail / samples_rank, 4) if a.variant == 'wf' else None,
+        'collectives': ({'backend': dist.get_backend(), 'world_size': world_size,
+                         'calls': ['gather (assemble_image, tiles) / reduce (samples)', 'all_reduce MAX (elapsed)',
+                                   'all_gather (per-rank rows)']} if pg else None),
         'medium_traversals_per_sample': round(M, 4),
         'pipeline_algorithmic_GBps': round(value * 1e6 * b_sample / 1e9, 3),
         'ranks': [{'rank': int(r[0]), 'rows': int(r[1]), 'samples': int(r[2]), 'render_s': round(r[3], 4),
@@ -470,7 +486,7 @@ def main():
             img = integ.tonemap(acc, total_spp).cpu().numpy()
             Image.fromarray(img).save(a.save_image)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTMI_ABI_VERSION 6
+#define PTMI_ABI_VERSION 7
 #define PTMI_MAX_IMAGES 16
 
 enum {
@@ -131,9 +131,13 @@ typedef struct ptmi_frame {
  * [3] paths ended by Russian roulette (kernels.py:1145-1157, the reference's
  * rr_paths_killed, fields.py:295), [4] paths ended by the depth / wave budget
  * (kernels.py:1139-1141, 1383; renderer.py:313: its max_depth_terminations,
- * fields.py:287). Accumulated with atomics; pass NULL to skip. [3] and [4]
- * since ABI v6 (the buffer must hold PTMI_NUM_COUNTERS entries). */
-#define PTMI_NUM_COUNTERS 5
+ * fields.py:287), [5] the part of [0] the wavefront traced in its one-launch
+ * tail (wf_drain; 0 for the megakernel), so per-kernel rates can attribute
+ * segments to the launch that traced them. Accumulated with atomics; pass
+ * NULL to skip. [3] and [4] since ABI v6, [5] since ABI v7 (the buffer must
+ * hold PTMI_NUM_COUNTERS entries). */
+#define PTMI_NUM_COUNTERS 6
+#define PTMI_COUNTER_TAIL_SEGMENTS 5
 
 /* Material class in a leaf code (bits 25-27), from the material flags:
  * constant-medium boundary; Perlin-textured Lambertian or isotropic; else by
@@ -228,6 +232,14 @@ size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
                    uint64_t *counters, void *stream);
+/* Schedule knob of ptmi_wf_render's tail (no effect on results): once a
+ * pipe's live slots fall below capacity / divisor (the work pool is then
+ * empty), one launch finishes its remaining paths and the items its slot
+ * groups still hold, instead of one intersect and one scatter launch per
+ * remaining wave. 0 = no tail launch; default 16. Process-wide, read at the
+ * start of each batch. Returns the previous divisor, or PTMI_EINVAL for a
+ * negative one. ABI v7. */
+int ptmi_wf_set_drain_at(int32_t divisor);
 
 /* Clears the accumulator's pixel set: kernels.clear_accum_buffer()
  * (kernels.py:1205-1209) / fields.clear_accumulation_buffer (fields.py:280). */

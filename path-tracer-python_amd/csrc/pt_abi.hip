@@ -2,8 +2,8 @@
 // include/ptmi.h): argument validation, scene/frame conversion, launch of the
 // megakernel / wavefront / tone-map / clear kernels. No device allocation
 // happens inside a render call; the megakernel calls are asynchronous and
-// graph-capturable, the wavefront reads its live-slot count back every 8
-// iterations (one pinned 4-byte slot, allocated once).
+// graph-capturable, the wavefront reads its live-slot counts back every 4
+// iterations (pinned 4-byte slots, allocated once).
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -314,6 +314,11 @@ int ptmi_wf_render(const ptmi_scene_view* scene, const ptmi_frame* frame, void* 
   return check_hip(wf_render(sc, fr, stack_needed(scene), workspace, workspace_bytes, accum, sample_begin,
                              sample_count, (unsigned long long*)counters, (hipStream_t)stream),
                    "wf_render");
+}
+
+int ptmi_wf_set_drain_at(int32_t divisor) {
+  if (divisor < 0) return fail(PTMI_EINVAL, "drain divisor must be >= 0");
+  return wf_set_drain_at(divisor);
 }
 
 int ptmi_clear(const ptmi_frame* frame, float* accum, void* stream) {

@@ -29,6 +29,8 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
                      float* accum, int32_t s_begin, int32_t s_count, unsigned long long* counters,
                      hipStream_t stream);
 size_t wf_workspace_bytes(int32_t npix, int32_t batch);
+// Sets the wavefront tail threshold (capacity / divisor; 0 = no tail launch); returns the previous one.
+int32_t wf_set_drain_at(int32_t divisor);
 // accum[pixel] += staging[s][p] for s = 0..batch-1 in order (profiled as `prof_kind`).
 hipError_t launch_stage_resolve(const DevFrame& fr, const float* staging, int32_t npix, int32_t batch,
                                 float* accum, int prof_kind, hipStream_t stream);

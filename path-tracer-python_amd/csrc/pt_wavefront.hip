@@ -45,12 +45,13 @@
 //     intersect -> scatter on its own stream, so
 //     the drain at the end of one pipe's launch is filled by another's (+21 %
 //     over one pipe).
-//   * THE TAIL: once a pipe's live count falls below capacity / 16 (the
-//     work pool is empty), one wf_drain launch finishes its remaining paths,
-//     each lane looping intersect -> shade over its own slot, instead of ~50
-//     nearly empty intersect + scatter launches;
+//   * THE TAIL: once a pipe's live count falls below capacity / 16
+//     (PTMI_WF_DRAIN_AT, or ptmi_wf_set_drain_at; the work pool is then
+//     empty), one wf_drain launch finishes its remaining paths and the items
+//     its groups still hold, each lane looping intersect -> shade over its
+//     own slot, instead of ~50 nearly empty intersect + scatter launches;
 //   * The host learns that a pipe has drained from a 4-byte live count read
-//     back every 8 iterations, and waits for chunk k's counts only after
+//     back every PTMI_WF_RB_CHUNK (4) iterations, and waits for chunk k's counts only after
 //     chunk k + 1 is queued, so no pipe idles through the host round trip
 //     (the reference reads its ray count back every bounce, renderer.py:315).
 //   * Each ray carries its own wave count and is dropped at max_depth waves,
@@ -65,6 +66,7 @@
 #include "pt_launch.hpp"
 #include "pt_prof.hpp"
 
+#include <atomic>
 #include <mutex>
 
 namespace ptmi {
@@ -802,18 +804,44 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
 }
 
 // The tail of a batch (wf_batch switches a pipe to it once its live slots fall
-// below PTMI_WF_DRAIN_AT of its capacity, i.e. after the work pool ran dry):
-// one launch finishes every path still in the pipe, each lane looping
-// intersect -> classify -> shade over its own slot until the path ends —
-// exactly the per-path steps of wf_intersect and wf_scatter (the same entry
-// functions, reading and writing the same slot), so every path, its draws,
-// its wave budget (Q14) and the counters are unchanged. What changes is the
-// schedule: instead of one intersect and one scatter launch per remaining
-// wave (~7.5 us each even when nearly empty, and ~50 of them for the longest
-// Russian-roulette survivors), the tail is one launch whose length is the
-// longest remaining path. Launched on the pipe's stream after a wf_scatter,
-// so no slot is fresh and the lists are not used; a pending slot finds no
-// work (the pool is empty) and is left alone.
+// below 1 / drain_at of its capacity, i.e. after the work pool ran dry: a
+// slot retires only when fetch_units finds every shard empty): one launch
+// finishes every path still in the pipe, each lane looping intersect ->
+// classify -> shade over its own slot until the path ends — exactly the
+// per-path steps of wf_intersect and wf_scatter (the same entry functions,
+// reading and writing the same slot), so every path, its draws, its wave
+// budget (Q14) and the counters are unchanged. The shards are empty, but a
+// group may still hold items it fetched and has not handed out yet
+// (wb.grp[g]: up to 63 of a single tail unit, more after a whole-chunk
+// fetch): a lane whose slot waits for work, or whose path ends, claims the
+// group's next item with an atomic on wb.grp[g].x and traces its camera ray
+// (generate_camera_rays, kernels.py:1219-1239) in the same loop, until the
+// group's range is spent. What changes is the schedule: instead of one
+// intersect and one scatter launch per remaining wave (~7.5 us each even when
+// nearly empty, and ~50 of them for the longest Russian-roulette survivors),
+// the tail is one launch whose length is the longest remaining chain of
+// paths of one slot. Launched on the pipe's stream after a wf_scatter, so no
+// slot is fresh and the lists are not used.
+__device__ __forceinline__ bool drain_claim(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& w, pt_v3& o,
+                                            pt_v3& d) {
+  int32_t* const nxt = &wb.grp[i >> 6].x;
+  const int32_t end = wb.grp[i >> 6].y;  // not changed by this launch
+  for (;;) {
+    const int32_t k = atomicAdd(nxt, 1);
+    if (k >= end) {
+      set_slot_item(wb.q, i, kDead);
+      return false;
+    }
+    const Item it = decode_item(fr, wb, (uint32_t)k);
+    if (!it.valid) continue;  // padding of a square outside the frame / past the batch
+    Rng rng{path_key(fr, wb, it), 0u};
+    get_ray(fr, it.px, it.py, rng, o, d);
+    w = (uint32_t)k | kFresh;  // wf_scatter's entry functions regenerate the ray from it (load_ray)
+    set_slot_item(wb.q, i, w);
+    return true;
+  }
+}
+
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, WfBufs wb,
                                                    unsigned long long* __restrict__ counters) {
@@ -823,22 +851,29 @@ __global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, W
   uint32_t n_seg = 0, n_med = 0, n_ended = 0, ends[2] = {0u, 0u};
   for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity;
        i += (int32_t)(gridDim.x * kWfBlock)) {
-    if (s_load(q.item + i) >= kPending) continue;  // retired, or waiting for work the pool no longer has
+    uint32_t w = s_load(q.item + i);
+    if (w == kDead) continue;  // retired: its group's items are all handed out
     for (;;) {
+      pt_v3 o, d;
+      if (w == kPending) {  // waiting for work: the group's next item, if any
+        if (!drain_claim(fr, wb, i, w, o, d)) break;
+      } else {
+        const float4 a = q_load(q.a + i);
+        const float2 dyz = h_load(q.d + i);
+        o = pt_v3f(a.x, a.y, a.z);
+        d = pt_v3f(a.w, dyz.x, dyz.y);
+      }
       // intersect_rays (kernels.py:1242-1263) for this slot
-      const float4 a = q_load(q.a + i);
-      const float2 dyz = h_load(q.d + i);
       float t = 0.0f;
       int32_t ref = 0;
-      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, pt_v3f(a.x, a.y, a.z), pt_v3f(a.w, dyz.x, dyz.y), kTMin,
-                                                       kTMax, st, t, ref);
+      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
       ++n_seg;
       if (!hit) ref = 0;
       h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
       const int32_t list = hit ? leaf_class(ref) : kListEnded;
       const uint32_t before = n_ended;
       if (list == kListEnded) {
-        end_unscattered(sc, fr, wb, i, s_load(q.item + i), ref);
+        end_unscattered(sc, fr, wb, i, w, ref);
         ++n_ended;
       } else if (list == kListMedium || list == kListNoise) {
         n_med += list == kListMedium ? 1u : 0u;
@@ -846,12 +881,15 @@ __global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, W
       } else {
         shade_entry(sc, fr, wb, list, i, n_ended, ends);
       }
-      if (n_ended != before) break;  // the path ended; its slot waits for work that will not come
+      // the path ended (its slot now waits for work), or continues from its
+      // stored ray (the item word holds the item without kFresh)
+      w = n_ended != before ? kPending : (w & ~kFresh);
     }
   }
   if (counters) {
     block_flush<2>({n_seg, n_med}, lds_stack, counters + 0);
     block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
+    block_flush<1>({n_seg}, lds_stack, counters + PTMI_COUNTER_TAIL_SEGMENTS);
   }
 }
 
@@ -893,15 +931,18 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
 #define PTMI_WF_RB_CHUNK 4  // A/B r04j: 4 +1.7 % C3, +1 % mesh fog over 8
 #endif
 #ifndef PTMI_WF_DRAIN_AT
-// A pipe whose read-back live count falls below capacity / PTMI_WF_DRAIN_AT
-// finishes its paths in one wf_drain launch (0 = never: one intersect and one
-// scatter launch per wave until the pipe is empty).
+// A pipe whose read-back live count falls below capacity / drain_at finishes
+// its paths in one wf_drain launch (0 = never: one intersect and one scatter
+// launch per wave until the pipe is empty). The default; ptmi_wf_set_drain_at
+// changes it at run time (tests drive the tail with 1: drain as soon as the
+// pool is dry, while most groups still hold fetched items).
 #define PTMI_WF_DRAIN_AT 16
 #endif
 #ifndef PTMI_WF_CAPACITY_LOG2
 #define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
 #endif
 constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
+std::atomic<int32_t> g_drain_at{PTMI_WF_DRAIN_AT};
 constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
 constexpr size_t kQueueBytesPerSlot = 48;
@@ -967,6 +1008,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
   for (int p = 0; p < kPipes; ++p) live[p] = true;
   int64_t it = 0;
   const int32_t chunk = PTMI_WF_RB_CHUNK;  // iterations between live-count readbacks
+  const int64_t drain_at = g_drain_at.load(std::memory_order_relaxed);
   hipError_t err = hipSuccess;
   // The host reads chunk k's live counts only after chunk k + 1 is queued, so
   // the pipes never idle through the readback's host round trip. Iterations
@@ -1013,9 +1055,10 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
       if (inflight[prev][p]) {
         const int32_t n_live = ps.pinned_live[prev * kPipes + p];
         live[p] = live[p] && n_live != 0;
-        if (live[p] && PTMI_WF_DRAIN_AT > 0 && (int64_t)n_live * PTMI_WF_DRAIN_AT < (int64_t)wbs[p].capacity) {
+        if (live[p] && drain_at > 0 && (int64_t)n_live * drain_at < (int64_t)wbs[p].capacity) {
           // the pool is empty (some slot found no work) and few paths are left:
-          // finish them in one launch, queued behind the iterations in flight
+          // finish them, and the items groups still hold, in one launch,
+          // queued behind the iterations in flight
           const int pd = prof_begin(kProfWfDrain, st[p]);
           hipLaunchKernelGGL((wf_drain<STACK, TRAV>), dim3((unsigned)(wbs[p].capacity / kWfBlock)), dim3(kWfBlock), 0,
                              st[p], sc, fr, wbs[p], counters);
@@ -1046,6 +1089,8 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
   if (err != hipSuccess) return err;
   return launch_stage_resolve(fr, wbs[0].staging, wbs[0].npix, batch, accum, kProfWfResolve, stream);
 }
+
+int32_t wf_set_drain_at(int32_t divisor) { return g_drain_at.exchange(divisor); }
 
 size_t wf_workspace_bytes(int32_t npix, int32_t batch) {
   if (npix <= 0 || batch <= 0) return 0;

@@ -11,9 +11,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PTMI_LIB') or os.path.join(_HERE, '_lib', 'libptmi.so')  # PTMI_LIB: A/B builds
-ABI_VERSION = 6  # PTMI_ABI_VERSION of include/ptmi.h
+ABI_VERSION = 7  # PTMI_ABI_VERSION of include/ptmi.h
 MAX_IMAGES = 16
-NUM_COUNTERS = 5
+NUM_COUNTERS = 6
+COUNTER_TAIL_SEGMENTS = 5  # wavefront segments traced in the tail launch (wf_drain), part of [0]
 
 PTMI_OK, PTMI_EINVAL, PTMI_ECAPACITY, PTMI_EHIP, PTMI_ENODEV = 0, -1, -2, -3, -4
 
@@ -56,7 +57,7 @@ TRAVERSALS = {'stack': 0, 'stackless': 1}
 EXPORTS = ('ptmi_version', 'ptmi_last_error', 'ptmi_scene_check', 'ptmi_mk_render', 'ptmi_mk_workspace_bytes',
            'ptmi_mk_render_ws', 'ptmi_mk_trace_ws', 'ptmi_mk_max_batch', 'ptmi_mk_resolve_ws', 'ptmi_wf_workspace_bytes',
            'ptmi_wf_render', 'ptmi_clear', 'ptmi_tonemap', 'ptmi_bvh_build_sah', 'ptmi_prof_start',
-           'ptmi_prof_stop', 'ptmi_prof_stop_busy', 'ptmi_node_bytes')
+           'ptmi_prof_stop', 'ptmi_prof_stop_busy', 'ptmi_node_bytes', 'ptmi_wf_set_drain_at')
 PROF_KINDS = ('megakernel', 'wf_generate', 'wf_intersect', 'wf_drain', 'wf_scatter', 'wf_resolve', 'mk_resolve')
 
 _lib = None
@@ -105,6 +106,7 @@ def load(path: str = LIB_PATH):
     lib.ptmi_wf_workspace_bytes.restype = C.c_size_t
     lib.ptmi_wf_render.argtypes = [C.POINTER(SceneView), C.POINTER(Frame), P, C.c_size_t, P, C.c_int32,
                                    C.c_int32, P, P]
+    lib.ptmi_wf_set_drain_at.argtypes = [C.c_int32]
     lib.ptmi_clear.argtypes = [C.POINTER(Frame), P, P]
     lib.ptmi_tonemap.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P]
     lib.ptmi_bvh_build_sah.argtypes = [P, C.c_int32, P, C.c_int32, P, C.c_int32, P, P, P, P, P, P, P,

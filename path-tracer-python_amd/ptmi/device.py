@@ -343,6 +343,15 @@ class Integrator:
         return {'segments': int(c[0]), 'medium': int(c[1]), 'paths': int(c[2]), 'rr': int(c[3]),
                 'depth_cap': int(c[4])}
 
+    def tail_segments(self):
+        """Segments the wavefront traced in its one-launch tail (wf_drain):
+        part of read_counters()['segments'], counted apart so per-kernel
+        rates attribute them to the launch that traced them."""
+        if self.counters is None:
+            return None
+        self._after_traces(torch.cuda.current_stream(self.scene.device))
+        return int(self.counters[_lib.COUNTER_TAIL_SEGMENTS].item())
+
     def reset_counters(self, stream=None):
         if self.counters is not None:
             s = stream if stream is not None else torch.cuda.current_stream(self.scene.device)

@@ -7,9 +7,8 @@ writes only accum[py, px]) and every path's random stream is keyed by
 exchange during rendering. Two partitions:
 
 * ``tiles``: interleaved row bands (band_rows rows, round-robin over ranks)
-  — every pixel is rendered entirely by one rank, so the gathered image is
-  bit-identical to a 1-GPU render; one sum-reduce of the f32 accumulator
-  (the other ranks' bands are zero) assembles it on the root.
+  — every pixel is rendered entirely by one rank, so the assembled image is
+  bit-identical to a 1-GPU render;
 * ``samples``: every rank renders the whole image for a disjoint set of
   sample indices (weak scaling: fixed work per GPU); the sum-reduce adds the
   partial accumulators (equal to the 1-GPU render up to f32 summation order).
@@ -17,12 +16,17 @@ exchange during rendering. Two partitions:
 Image assembly is one collective per render (RCCL over xGMI on MI355X; gloo
 in the CPU tests), ``assemble_image``:
 * tiles: a ``gather`` of each rank's owned row bands onto the root (no
-  arithmetic, so the image is bit-identical to one GPU; each non-root rank
-  sends only its own rows, W*rows*12 bytes: 7.7 MB / 8 at 800x800, 99.5 MB / 8
-  at 3840x2160, instead of reducing a full-frame accumulator that is 7/8
-  zeros);
+  arithmetic, so the image is bit-identical to one GPU; each rank sends only
+  its own rows, W*rows*12 bytes: 7.7 MB / 8 at 800x800, 99.5 MB / 8 at
+  3840x2160, instead of reducing a full-frame accumulator that is 7/8 zeros);
 * samples: a sum-``reduce`` of the full accumulators (every rank holds every
   pixel).
+
+Every collective here runs whenever a process group is initialised, at world
+size 1 too (a gather / reduce / all-reduce / all-gather over one rank), so
+``bench.py --gpus 1 --dist-backend nccl`` and tests/test_gpu_rccl.py execute
+the exact RCCL calls of an N-GPU run on the one GPU of a test box. Without a
+process group they are no-ops.
 """
 from __future__ import annotations
 
@@ -72,11 +76,24 @@ class Shard:
         return [r for r in range(height) if (r // b) % s == o]
 
 
-def reduce_accum(accum, dst=0, group=None):
-    """Sum-reduce the accumulator onto `dst` (in place); no-op for world 1."""
+def _initialized():
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        if accum.is_cuda and dist.get_backend(group) == 'gloo':  # rehearsal backend: reduce a host copy
+    return dist.is_available() and dist.is_initialized()
+
+
+def _host_staged(t, group=None):
+    """gloo is only the multi-rank rehearsal backend: it reduces / gathers
+    host tensors, so device tensors go through a host copy."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == 'gloo'
+
+
+def reduce_accum(accum, dst=0, group=None):
+    """Sum-reduce the accumulator onto `dst` (in place); no-op without a
+    process group."""
+    import torch.distributed as dist
+    if _initialized():
+        if _host_staged(accum, group):
             host = accum.cpu()
             dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM, group=group)
             accum.copy_(host)
@@ -88,7 +105,7 @@ def reduce_accum(accum, dst=0, group=None):
 def max_over_ranks(value, device=None, group=None):
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    if not _initialized():
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -103,10 +120,11 @@ def assemble_image(accum, shard, dst=0, group=None):
     (max_rows, W, 3) buffer (max_rows = the largest rank share, so every
     gather buffer has one shape) and one ``gather`` brings them to the root,
     which writes them into its accumulator. samples: ``reduce_accum``.
-    No-op for world 1."""
+    No-op without a process group; with one, the collective runs at every
+    world size (at world 1 the root gathers its own rows)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) <= 1:
+    if not _initialized():
         return accum
     if shard.mode != 'tiles':
         return reduce_accum(accum, dst, group)
@@ -114,8 +132,7 @@ def assemble_image(accum, shard, dst=0, group=None):
     H = accum.shape[0]
     rows_of = [Shard(r, world, 'tiles', shard.band_rows).rows(H) for r in range(world)]
     max_rows = max(len(r) for r in rows_of)
-    host = accum.is_cuda and dist.get_backend(group) == 'gloo'  # rehearsal backend: host buffers
-    dev = torch.device('cpu') if host else accum.device
+    dev = torch.device('cpu') if _host_staged(accum, group) else accum.device
     mine = torch.tensor(rows_of[rank], dtype=torch.long, device=accum.device)
     send = torch.zeros((max_rows,) + tuple(accum.shape[1:]), dtype=accum.dtype, device=accum.device)
     send[:len(rows_of[rank])] = accum.index_select(0, mine)
@@ -128,3 +145,16 @@ def assemble_image(accum, shard, dst=0, group=None):
                 idx = torch.tensor(rows_of[r], dtype=torch.long, device=accum.device)
                 accum.index_copy_(0, idx, recv[r][:len(rows_of[r])].to(accum.device))
     return accum
+
+
+def gather_ranks(vals, device=None, group=None):
+    """Per-rank float rows (one ``all_gather`` of float64) -> list of lists,
+    rank order; [vals] without a process group."""
+    import torch
+    import torch.distributed as dist
+    if not _initialized():
+        return [list(vals)]
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return [o.cpu().tolist() for o in out]

@@ -254,23 +254,32 @@ class MI355XRenderer:
 
     def _get_rr_stats(self):
         """Russian-roulette statistics of the last render (renderer.py:481-500)
-        from the device counters.
+        from the device counters, with the reference's keys, value types and
+        formulas, so a drop-in caller can format or add them.
 
-        Schema: the reference's keys, plus 'paths' and 'depth_cap'.
-        * 'killed': paths ended by RR (kernels.py:1145-1157), counted exactly.
-        * 'survived', 'total_rr_paths', 'avg_depth_killed',
-          'avg_depth_survived': None. The device does not count paths that
-          reached depth 3 unkilled, nor depth sums (kernels.py:1200-1202
-          define them). In the reference they are always 0, because the
-          atomics that would fill them are commented out (kernels.py:1189-1202).
-        * 'kill_rate': killed / all paths x 100. The reference divides by
-          killed + survived, which cannot be formed without 'survived'."""
+        * 'killed': paths ended by RR (kernels.py:1145-1157), counted exactly
+          (the reference's atomics are commented out, kernels.py:1193-1202,
+          so its own 'killed' is always 0).
+        * 'survived', 'avg_depth_killed', 'avg_depth_survived': 0 / 0.0, as in
+          the reference: the device does not count paths that passed the RR
+          test, nor depth sums. Their names are listed under 'uncounted'.
+        * 'total_rr_paths' = killed + survived and 'kill_rate' = killed /
+          total_rr_paths x 100 (0.0 when empty): the reference's formulas
+          (renderer.py:488-489), so with survived uncounted 'kill_rate' is 100
+          whenever anything was killed. 'kill_rate_of_paths' = killed / all
+          paths x 100 is the informative rate.
+        * Extra keys: 'paths', 'depth_cap' (paths ended by the depth / wave
+          budget), 'uncounted'."""
         c = self.integrator.read_counters() or {}
-        killed = c.get('rr', 0)
-        return {'killed': killed, 'survived': None, 'total_rr_paths': None,
-                'kill_rate': 100.0 * killed / c['paths'] if c.get('paths') else 0.0,
-                'avg_depth_killed': None, 'avg_depth_survived': None,
-                'paths': c.get('paths', 0), 'depth_cap': c.get('depth_cap', 0)}
+        killed, survived = int(c.get('rr', 0)), 0
+        total = killed + survived
+        paths = int(c.get('paths', 0))
+        return {'killed': killed, 'survived': survived, 'total_rr_paths': total,
+                'kill_rate': (killed / total * 100) if total > 0 else 0.0,
+                'avg_depth_killed': 0.0, 'avg_depth_survived': 0.0,
+                'kill_rate_of_paths': 100.0 * killed / paths if paths else 0.0,
+                'paths': paths, 'depth_cap': int(c.get('depth_cap', 0)),
+                'uncounted': ('survived', 'avg_depth_killed', 'avg_depth_survived')}
 
     def _get_average_depth(self):
         """Mean ray segments per path (renderer.py:473-479 reports the mean

@@ -2,9 +2,11 @@
 
 Each rank renders its shard with the CPU oracle standing in for its GPU (the
 kernels themselves are covered by the -m gpu parity tests) and the product's
-ptmi.distributed.reduce_accum assembles the image on rank 0:
-  * tiles   -> bit-identical to the single-device render,
-  * samples -> equal up to f32 summation order.
+ptmi.distributed.assemble_image (the collective bench.py times) assembles
+the image on rank 0:
+  * tiles   -> a gather of owned row bands, bit-identical to the
+               single-device render,
+  * samples -> a sum-reduce, equal up to f32 summation order.
 bench.py's own bookkeeping (balanced bands, the band gather it times,
 gather_ranks, value) is run at world sizes 2, 4 and 8.
 """
@@ -37,7 +39,7 @@ def _worker(rank, world, port, mode, out_path):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from parity_helpers import oracle_render
     from ptmi import device
-    from ptmi.distributed import Shard, reduce_accum
+    from ptmi.distributed import Shard, assemble_image
     sh = Shard(rank, world, mode, band_rows=8)
     H = WIDTH
     acc = np.zeros((H, WIDTH, 3), np.float32)
@@ -48,7 +50,7 @@ def _worker(rank, world, port, mode, out_path):
         for r in rows:  # accumulate in place: same per-pixel float order as one device
             oracle_render(SCENE, WIDTH, 'mk', (0, r, WIDTH, 1), b, c, threads=1, acc=acc)
     t = torch.from_numpy(acc)
-    reduce_accum(t, dst=0)
+    assemble_image(t, sh, dst=0)
     if rank == 0:
         np.save(out_path, t.numpy())
     dist.destroy_process_group()
@@ -187,3 +189,51 @@ def test_bench_tiles_bookkeeping_at_scale(tmp_path, world, height):
     assert rec['elapsed'] == want_elapsed
     assert rec['value'] == width * height * rec['spp'] / want_elapsed / 1e6
     assert rec['scaling'] == 'strong' and 'gather of owned row bands' in rec['parallelism']
+
+
+def _world_one_worker(rank, world, port, out_path):
+    """A process group of one rank (bench.py --gpus 1 --dist-backend ...):
+    every collective of the N-rank flow runs — the gather of assemble_image
+    (tiles), its sum-reduce (samples), gather_ranks' all_gather and
+    max_over_ranks' all_reduce — and leaves the one-rank values unchanged."""
+    import json
+    import sys
+    for p in (ROOT, os.path.join(ROOT, 'path-tracer-python_amd'), os.path.join(ROOT, 'tests')):
+        sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import bench
+    from ptmi.distributed import Shard, assemble_image, max_over_ranks
+    a = bench.parse(['--preset', 'c2', '--gpus', '1', '--dist-backend', 'gloo'])
+    img = np.random.default_rng(3).standard_normal((37, 5, 3)).astype(np.float32)
+    res = {'process_group': a.process_group, 'backend': a.dist_backend}
+    for mode in ('tiles', 'samples'):
+        sh = Shard.balanced(0, 1, mode, 37)
+        t = torch.from_numpy(img.copy())
+        assemble_image(t, sh, dst=0)
+        res[mode] = bool(np.array_equal(t.numpy(), img))
+    res['ranks'] = bench.gather_ranks([0, 37, 2.5], 'cpu', 1)
+    res['max'] = max_over_ranks(1.25)
+    with open(out_path, 'w') as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_collectives_run_at_world_size_one(tmp_path):
+    import json
+    out = str(tmp_path / 'w1.json')
+    mp.start_processes(_world_one_worker, args=(1, _free_port(), out), nprocs=1, start_method='spawn')
+    with open(out) as f:
+        rec = json.load(f)
+    assert rec['process_group'] is True and rec['backend'] == 'gloo'
+    assert rec['tiles'] and rec['samples']
+    assert rec['ranks'] == [[0.0, 37.0, 2.5]] and rec['max'] == 1.25
+
+
+def test_bench_process_group_flag():
+    import bench
+    assert bench.parse(['--gpus', '1']).process_group is False
+    assert bench.parse(['--gpus', '1', '--dist-backend', 'nccl']).process_group is True
+    a = bench.parse(['--gpus', '2'])
+    assert a.process_group is True and a.dist_backend == 'nccl'

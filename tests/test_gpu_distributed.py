@@ -1,9 +1,12 @@
 """GPU: the multi-GPU partition end to end with the HIP integrators, two ranks
 sharing the box's one GPU over gloo (RCCL needs one GPU per rank; the driver's
-8-GPU run uses it). Each rank renders its shard through the C-ABI and the
-product's ptmi.distributed.reduce_accum assembles the image on rank 0:
-  * tiles   -> bit-identical to a one-rank render of the same samples,
-  * samples -> equal to it up to f32 summation order.
+8-GPU run uses it; tests/test_gpu_rccl.py runs the same collectives on RCCL at
+world size 1). Each rank renders its shard through the C-ABI into a CUDA
+accumulator and the product's ptmi.distributed.assemble_image — the collective
+bench.py times, here through its gloo host-staging branch — assembles the
+image on rank 0:
+  * tiles   -> gather of owned rows, bit-identical to a one-rank render,
+  * samples -> sum-reduce, equal to it up to f32 summation order.
 Mirrors tests/test_distributed_gloo.py, which runs the same flow on the CPU oracle."""
 import os
 import socket
@@ -34,7 +37,7 @@ def _worker(rank, world, port, mode, variant, out_path):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from parity_helpers import scene_inputs
     from ptmi import device
-    from ptmi.distributed import Shard, reduce_accum
+    from ptmi.distributed import Shard, assemble_image
     sa, cam, bg = scene_inputs(SCENE, WIDTH)
     W, H = cam['width'], cam['height']
     integ = device.Integrator(device.DeviceScene.from_arrays(sa))
@@ -46,7 +49,7 @@ def _worker(rank, world, port, mode, variant, out_path):
         b, c = sh.sample_range(k, SPS)
         render(fr, acc, b, c)
     torch.cuda.synchronize()
-    reduce_accum(acc, dst=0)
+    assemble_image(acc, sh, dst=0)
     if rank == 0:
         np.save(out_path, acc.cpu().numpy())
     dist.destroy_process_group()

@@ -314,3 +314,58 @@ def test_wavefront_tail_runs_in_one_drain_launch_per_pipe():
     linf, exact = compare(acc.cpu().numpy(), ref, 8)
     assert linf <= 1e-4 and exact >= 0.999
     assert integ.read_counters() == ost
+
+
+_FULL_FRAME_ORACLE = {}
+
+
+@pytest.mark.parametrize('drain_at', [1, 2, 0])
+def test_wavefront_tail_traces_the_items_groups_still_hold(drain_at):
+    """the tail launch starts once a pipe's live slots fall
+    below capacity / drain_at, which only says the shards are empty — a
+    64-slot group may still hold items it fetched and has not handed out
+    (wb.grp). wf_drain must trace those too. The whole 800x800 frame x 4 spp
+    is 2.56 M items for 2^21 queue slots, so the tail begins while groups
+    hold items; drain_at = 1 starts it as soon as the pool is dry (most
+    groups then hold some), 2 half-way, 0 never (one intersect + scatter
+    launch per wave to the end). Every path is traced exactly once: the
+    paths counter is W x H x spp, the image and the counters equal the
+    oracle's bit for bit, and the tail traced segments whenever it ran."""
+    import torch
+    from parity_helpers import compare, oracle_render
+    from ptmi import device, _lib
+    sa, cam, bg = scene_inputs('vol2_final_scene', 800)
+    W, H, spp = cam['width'], cam['height'], 4
+    lib = _lib.load()
+    integ = device.Integrator(device.DeviceScene.from_arrays(sa))
+    fr = device.make_frame(cam, bg, 50, 0, W, H)
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device='cuda')
+    integ.reset_counters()
+    prev = lib.ptmi_wf_set_drain_at(drain_at)
+    assert prev == 16
+    try:
+        with _lib.KernelTimer(max_launches=100000) as kt:
+            integ.render_wf(fr, acc, 3, spp)
+            torch.cuda.synchronize()
+    finally:
+        assert lib.ptmi_wf_set_drain_at(prev) == drain_at
+    gst, tail = integ.read_counters(), integ.tail_segments()
+    drains = kt.result['wf_drain']['launches']
+    assert gst['paths'] == W * H * spp
+    if drain_at:
+        assert 1 <= drains <= 4 and tail > 0
+    else:
+        assert drains == 0 and tail == 0
+    if 'ref' not in _FULL_FRAME_ORACLE:
+        _FULL_FRAME_ORACLE['ref'] = oracle_render('vol2_final_scene', 800, 'wf', (0, 0, W, H), 3, spp)
+    ref, ost = _FULL_FRAME_ORACLE['ref']
+    linf, exact = compare(acc.cpu().numpy(), ref, spp)
+    assert linf == 0.0 and exact == 1.0
+    assert gst == ost
+
+
+def test_drain_divisor_is_validated():
+    from ptmi import _lib
+    lib = _lib.load()
+    assert lib.ptmi_wf_set_drain_at(-1) == _lib.PTMI_EINVAL
+    assert lib.ptmi_wf_set_drain_at(16) == 16

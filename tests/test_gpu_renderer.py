@@ -221,9 +221,15 @@ def test_rr_statistics_match_the_oracle(tmp_path):
     _, ost = oracle_render('wavefront_comparison', 400, 'mk', (0, 0, 400, 225), 0, 4)
     assert st['killed'] == ost['rr'] > 0 and st['depth_cap'] == ost['depth_cap']
     assert st['paths'] == ost['paths'] == 400 * 225 * 4
-    # the reference's keys (renderer.py:493-500); what the device does not count is None
-    assert {'killed', 'survived', 'total_rr_paths', 'kill_rate', 'avg_depth_killed',
-            'avg_depth_survived'} <= set(st)
-    assert st['survived'] is None and st['kill_rate'] == 100.0 * st['killed'] / st['paths']
+    # the reference's keys and value types (renderer.py:493-500): numbers a
+    # caller can format or add; what the device does not count is 0, as in the
+    # reference (its atomics are commented out, kernels.py:1193-1202)
+    keys = ('killed', 'survived', 'total_rr_paths', 'kill_rate', 'avg_depth_killed', 'avg_depth_survived')
+    assert set(keys) <= set(st) and all(isinstance(st[k], (int, float)) for k in keys)
+    assert st['survived'] == 0 and st['avg_depth_killed'] == 0.0 and st['avg_depth_survived'] == 0.0
+    assert st['total_rr_paths'] == st['killed'] and st['kill_rate'] == 100.0  # the reference's formula
+    assert st['kill_rate_of_paths'] == 100.0 * st['killed'] / st['paths']
+    assert set(st['uncounted']) == {'survived', 'avg_depth_killed', 'avg_depth_survived'}
+    sum(st[k] for k in keys)  # a drop-in caller adding them must not raise
     r.setup_live_preview(250)  # GUI hooks: headless no-ops
     assert r.update_preview_if_needed() is None
