@@ -3,17 +3,36 @@
 // Replaces the wavefront stage kernels of kernels.py:1219-1418 as driven by
 // TaichiRenderer.render_wavefront (renderer.py:305-334). Stages and layout
 // are designed for CDNA4, not translated:
-//   * ray queue = five streams per slot (A = o.xyz,d.x; D = d.yz; C =
-//     thr.xyz, meta; the work-item word; the rng draw counter), each read
-//     only by the stage that needs it, every access a coalesced per-lane
-//     vector load/store; meta = depth | wave << 8. wf_intersect reads the
-//     item word and the ray (24 B); a fresh camera ray is not stored at all
-//     (wf_scatter regenerates it from its item);
+//   * RAY BUFFERS, COMPACTED AND SORTED BY DIRECTION (round 5): every
+//     iteration traces up to `capacity` rays per pipe from one of two ray
+//     buffers (by iteration parity). The rays that continue are written by
+//     wf_scatter into the other buffer, appended (wave64 ballot + one atomic
+//     per wave and bin) to the segment of their direction octant, so one
+//     wf_intersect wave traces 64 rays of one octant that left neighbouring
+//     surfaces (one wf_scatter wave's worth of shading): the traversal visits
+//     similar nodes in the same order across the wave. Segments are also
+//     sharded by the producing block's XCD (8 shards), so the appends of one
+//     launch spread over 64 counters; a wave reads all 64 counts at once and
+//     maps its work index to (bin, shard, offset) with a scan. A segment that
+//     overflows its region spills into an unsorted overflow region. The
+//     reference appends continuing rays to one next queue with one atomic per
+//     ray and copies it back (kernels.py:1377-1418);
+//   * FRESH CAMERA RAYS fill the buffer back up to `capacity` every
+//     iteration: the lanes past the continuing rays claim consecutive work
+//     items (one 8x8 pixel square x one sample per 64 items) with one atomic
+//     per wave on their XCD's shard of the work pool (stealing from the other
+//     shards when it is empty) and trace their camera rays
+//     (generate_camera_rays, kernels.py:1219-1239); a fresh ray is not
+//     stored, only its item word (| kFresh): wf_scatter regenerates it;
+//   * ray record = five streams (A = o.xyz,d.x; D = d.yz; C = thr.xyz, meta;
+//     the work-item word; the rng draw counter), each read only by the stage
+//     that needs it, every access a per-lane vector load/store, coalesced
+//     along a segment; meta = depth | wave << 8;
 //   * hit record = 8 B (t, leaf ref); hit point and normal are recomputed in
 //     the shading kernel with the reference's own expressions;
 //   * CLOSEST-HIT CLASSIFICATION: wf_intersect ends the paths a hit or miss
 //     ends without a scatter (miss: shade_miss_rays, kernels.py:1266-1280;
-//     emissive: kernels.py:1365-1375) and compacts every other slot, by its
+//     emissive: kernels.py:1365-1375) and compacts every other ray, by its
 //     hit's material, into one of five lists with wave64 ballot + mbcnt (one
 //     atomic per wave and list): Lambertian, metal/isotropic, dielectric,
 //     constant-medium boundary, Perlin-textured surface;
@@ -25,35 +44,27 @@
 //     material's scatter (kernels.py:817-917). Separate launches per material
 //     lost 6 %, separate shading and medium launches 5 %: a launch costs
 //     ~7.5 us per pipe and iteration even when its lists are empty;
-//   * WORK POOL, IN-PLACE SLOTS: the reference pushes one sample of every
-//     pixel through max_depth bounce-synchronous waves (renderer.py:305-334)
-//     and compacts survivors into a next queue with one atomic per ray, so
-//     after a few bounces its queues are nearly empty. Here the (sample,
-//     pixel) pairs of a batch are work items: a queue slot keeps its ray in
-//     place from bounce to bounce (no append, no swap copy: kernels.py:
-//     1402-1418 removed) and, when the path ends, waits for the next
-//     wf_intersect, which hands it the camera ray of the next work item — so
-//     every launch works on a full queue until the batch runs out.
-//   * Work is handed out per 64-slot group (one wave): a group draws 64-item
-//     units (one 8x8 pixel square x one sample) in chunks of a few samples of
-//     the same square, so a wave's rays stay coherent. Unit counters are
-//     sharded 8 ways by slot block (blocks b and b+8 share an XCD), one
-//     atomic per chunk, each counter on its own 256-B line, because a single
-//     device-wide counter saturates near 88 returning atomics/us on MI355X
-//     (MI355X_MICROARCH.md, "dequeue") and was measured at 97 % wait cycles.
-//   * PIPES: the queue is split into 4 independent parts, each looping
-//     intersect -> scatter on its own stream, so
-//     the drain at the end of one pipe's launch is filled by another's (+21 %
-//     over one pipe).
-//   * THE TAIL: once a pipe's live count falls below capacity / 16
-//     (PTMI_WF_DRAIN_AT, or ptmi_wf_set_drain_at; the work pool is then
-//     empty), one wf_drain launch finishes its remaining paths and the items
-//     its groups still hold, each lane looping intersect -> shade over its
-//     own slot, instead of ~50 nearly empty intersect + scatter launches;
-//   * The host learns that a pipe has drained from a 4-byte live count read
-//     back every PTMI_WF_RB_CHUNK (4) iterations, and waits for chunk k's counts only after
-//     chunk k + 1 is queued, so no pipe idles through the host round trip
-//     (the reference reads its ray count back every bounce, renderer.py:315).
+//   * WORK POOL: the reference pushes one sample of every pixel through
+//     max_depth bounce-synchronous waves (renderer.py:305-334), so after a
+//     few bounces its queues are nearly empty. Here the (sample, pixel)
+//     pairs of a batch are work items, handed out as rays end, so every
+//     launch works on a full buffer until the batch runs out. Item counters
+//     are sharded 8 ways (blocks b and b+8 share an XCD), each counter on its
+//     own 256-B line, because a single device-wide counter saturates near 88
+//     returning atomics/us on MI355X (MI355X_MICROARCH.md, "dequeue");
+//   * PIPES: the rays are split into 4 independent parts, each looping
+//     intersect -> scatter on its own stream, so the drain at the end of one
+//     pipe's launch is filled by another's (+21 % over one pipe);
+//   * THE TAIL: once the pool is empty and a pipe traces fewer than
+//     capacity / 16 rays per iteration (PTMI_WF_DRAIN_AT, or
+//     ptmi_wf_set_drain_at), one wf_drain launch finishes its remaining
+//     paths, each lane looping intersect -> scatter over its own ray, instead
+//     of ~50 nearly empty intersect + scatter launches;
+//   * The host learns that a pipe has drained from its status word (rays
+//     traced, pool empty) read back every PTMI_WF_RB_CHUNK (4) iterations,
+//     and waits for chunk k's status only after chunk k + 1 is queued, so no
+//     pipe idles through the host round trip (the reference reads its ray
+//     count back every bounce, renderer.py:315).
 //   * Each ray carries its own wave count and is dropped at max_depth waves,
 //     exactly the reference's per-path budget (Q14, incl. passthrough Q11).
 //   * A path adds at most one colour to its pixel, when it ends (a miss, or an
@@ -62,7 +73,8 @@
 //     [sample][pixel]; a resolve kernel then adds the slots into the
 //     accumulator in sample order — the same float additions, in the same
 //     order, as the reference's per-sample accumulation, with no atomics and
-//     no ordering constraint between concurrent paths of one pixel.
+//     no ordering constraint between concurrent paths of one pixel. Which
+//     ray is traced in which lane, and when, therefore changes nothing.
 #include "pt_launch.hpp"
 #include "pt_prof.hpp"
 
@@ -74,9 +86,6 @@ namespace ptmi {
 constexpr int kShards = 8;
 #ifndef PTMI_WF_CHUNK_SAMPLES
 #define PTMI_WF_CHUNK_SAMPLES 4  // samples per work chunk (one 8x8 pixel square each)
-#endif
-#ifndef PTMI_WF_TAIL
-#define PTMI_WF_TAIL 2  // a shard hands out single units once it has < TAIL chunks per group left
 #endif
 #ifndef PTMI_WF_BLOCK
 #define PTMI_WF_BLOCK 128  // threads per block of the queue kernels (A/B on MI355X, parity-identical: 128 vs 256
@@ -109,30 +118,47 @@ constexpr int isect_lds() {
 #ifndef PTMI_WF_MAX_BLOCKS
 #define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together; A/B: 4096 -1.5 %, 8192 -3.5 % (C3)
 #endif
-constexpr uint32_t kDead = 0xffffffffu;     // item of a retired slot
-constexpr uint32_t kPending = 0xfffffffeu;  // item of a slot waiting for work (assigned in wf_intersect)
-// A slot whose camera ray was generated and traced in this iteration's
-// wf_intersect holds its item | kFresh and nothing else: the ray is not
-// stored, wf_scatter regenerates it from the item (get_ray, kernels.py:
-// 176-201: the same draws from the same counter-based stream), with
-// throughput 1 and depth 0. Items are < 2^31 (wf_render bounds them).
+// A fresh camera ray (generated and traced in this iteration's wf_intersect)
+// is stored as its item | kFresh and nothing else: wf_scatter regenerates it
+// from the item (get_ray, kernels.py:176-201: the same draws from the same
+// counter-based stream), with throughput 1 and depth 0. Items are < 2^31
+// (wf_render bounds them).
 constexpr uint32_t kFresh = 0x80000000u;
 
-// Ray queue: five streams per slot, each read only by the stage that needs
-// it. wf_intersect reads the item word (4 B) of every slot and the ray
-// (o, d: A + D, 24 B) of a traced one; wf_scatter reads the rest.
-struct Queue {
-  float4* a;      // o.xyz, d.x
-  float2* d;      // d.y, d.z
-  float4* c;      // thr.xyz, meta (bits)
-  uint32_t* item; // work item (| kFresh), kPending or kDead
-  uint32_t* ctr;  // rng draw counter
+// Continuing-ray segments: kBins direction bins x kShards producer shards,
+// one counter each (kSegs <= 64: one wave holds them all, one per lane).
+// PTMI_WF_BINS 1 keeps the compaction without the sort. A/B on MI355X
+// (round 5, parity-identical; profiles/r05/ab/ab_wf_sort.log): against the
+// round-4 in-place slots (1685-1694 Msamples/s on C3, 705-708 on mesh fog)
+// the compacted buffers alone give 1889-1900 / 847-849, sorted by octant
+// 1914-1923 / 850-854; wf_intersect's lane efficiency 0.43 unsorted, 0.45
+// sorted (round 4: 0.32; profiles/r05/pmc/).
+#ifndef PTMI_WF_BINS
+#define PTMI_WF_BINS 8
+#endif
+constexpr int kBins = PTMI_WF_BINS;
+static_assert(kBins == 1 || kBins == 8, "direction bins: 1 (unsorted) or the 8 octants");
+constexpr int kSegs = kBins * kShards;
+#ifndef PTMI_WF_SEG_DIV
+#define PTMI_WF_SEG_DIV 16  // a segment's region holds capacity / this rays (4x an even share of 64 segments)
+#endif
+
+// Ray buffer of one iteration parity: positions [0, npos) of six streams.
+// Segment s holds positions [s * seg_cap, (s + 1) * seg_cap), the overflow
+// region the next `capacity`, the fresh camera rays the last `capacity`.
+struct RayBuf {
+  float4* a;       // o.xyz, d.x
+  float4* c;       // thr.xyz, meta (bits)
+  float2* d;       // d.y, d.z
+  float2* hit;     // t, leaf ref (bits) of the closest hit (wf_intersect -> wf_scatter)
+  uint32_t* item;  // work item (| kFresh)
+  uint32_t* ctr;   // rng draw counter
 };
 
 // Closest-hit lists (wf_intersect fills them, wf_scatter drains them).
-// Each list holds kShards segments of medseg slot indices; the medium and
+// Each list holds kShards segments of medseg ray positions; the medium and
 // Perlin lists share one array, the Perlin one filling its segments from the
-// top (a slot is in at most one list, so together they never exceed a segment).
+// top (a ray is in at most one list, so together they never exceed a segment).
 // Misses and emissive hits (class kListEnded) end in wf_intersect: a lane
 // that finishes its traversal early ends its path while the wave's longest
 // traversal runs, nearly for free. A/B on MI355X (round 4): an ended list
@@ -142,31 +168,29 @@ enum : int32_t { kListLambertian = 0, kListGlossy = 1, kListDielectric = 2, kLis
                  kListEnded = 5, kLists = 5 };
 
 struct WfBufs {
-  Queue q;
-  float2* hit;        // t, leaf ref (bits) of a traced slot's closest hit; ref 0 for a miss
-  int32_t* lists;     // 4 arrays of capacity indices: Lambertian, glossy + ended, dielectric, medium + Perlin
+  RayBuf rb[2];       // by iteration parity: wf_intersect(k) and wf_scatter(k) read rb[k & 1], wf_scatter(k) writes rb[(k + 1) & 1]
+  int32_t* lists;     // 4 arrays of kShards x medseg positions: Lambertian, glossy, dielectric, medium + Perlin
   float* staging;     // [batch][npix][3] path colours
   int32_t* ctl;       // this pipe's counters, one per 256-B line (see ctl_*)
   char* spill;        // this pipe's spilled stack slots of wf_intersect (kSpillSlots rows of its grid's threads)
-  int32_t* next;      // next-unit counters shared by the pipes, one per 256-B line
-  int32_t capacity;   // queue slots (multiple of kShards * kWfBlock)
-  int32_t medseg;     // slots per shard
-  int2* grp;          // per 64-slot group (one wave in wf_intersect): {next item, end} of its fetched units
+  int32_t* next;      // next-item counters of the work pool shards, shared by the pipes, one per 256-B line
+  int32_t capacity;   // rays traced per iteration (this pipe)
+  int32_t seg_cap;    // positions per continuing-ray segment
+  int32_t medseg;     // positions per shard segment of a material list
   int32_t npix;       // pixels of the frame's pixel set
   int32_t sq_x, nsq;  // 8x8 pixel squares covering the pixel set: per row, total
   int32_t csamp;      // samples per chunk: a chunk is one square x csamp samples (64 * csamp items)
   int32_t batch;      // samples of the batch
-  int32_t nunits;     // 64-item units of the batch (one square x one sample; csamp per chunk)
-  int32_t shard_len;  // units per shard (a multiple of csamp): shard s owns [s*len, min((s+1)*len, nunits))
-  int32_t shard_groups; // 64-slot groups drawing from each shard
+  int32_t nitems;     // work items of the batch, padded to whole squares and chunks
+  int32_t shard_len;  // items per pool shard (whole chunks): shard s owns [s*len, min((s+1)*len, nitems))
   int32_t s_begin;    // first sample of the batch
   FastDiv by_per, by_nsq, by_sqx;  // item decode: / (64 * csamp), / nsq, / sq_x
 };
 
-// Pipes: the queue is split into PTMI_WF_PIPES independent halves, each
-// driven through its own intersect/shade/medium loop on its own stream, so
-// one pipe's kernels fill the drain at the end of the other's. They share the
-// work pool (next-unit counters) and the staging buffer.
+// Pipes: the rays are split into PTMI_WF_PIPES independent parts, each
+// driven through its own intersect/scatter loop on its own stream, so one
+// pipe's kernels fill the drain at the end of another's. They share the work
+// pool (next-item counters) and the staging buffer.
 #ifndef PTMI_WF_PIPES
 #define PTMI_WF_PIPES 4  // A/B on MI355X: 1 -> 2 pipes +15 % (C3), 2 -> 4 +5 %
 #endif
@@ -174,49 +198,60 @@ constexpr int32_t kPipes = PTMI_WF_PIPES;
 
 // Device-scope atomics are performed per cache line at the memory side, so
 // counters sharing a line serialize as one: every counter gets its own
-// 256-B line. Lines 0-7: next unit per shard (shared); then per pipe 81
-// lines: live slots (read by the host), and two sets (by iteration parity)
-// of one count per list and shard. wf_intersect of iteration k appends to set
-// k & 1 and wf_scatter reads it and zeroes set (k + 1) & 1 for the next
-// iteration's wf_intersect.
+// 256-B line. Lines 0-7: next item per pool shard (shared); then per pipe:
+// its status ([2]: the pool was empty after the last wf_scatter's iteration,
+// written by that wf_scatter; [0], [1]: the continuing rays of the last
+// wf_intersect and the [2] it saw, for the host), two sets (by
+// iteration parity) of kSegs segment counts and one overflow count, and two
+// sets of one count per material list and shard.
 constexpr int32_t kLine = 64;
-constexpr int32_t kPipeLines = 1 + 2 * kLists * 8;
+constexpr int32_t kPipeLines = 3 + 2 * kSegs + 2 * kLists * kShards;
 constexpr int32_t kCtlWords = (8 + kPipeLines * kPipes) * kLine;
 __host__ __device__ __forceinline__ int32_t* ctl_next(const WfBufs& wb, int32_t s) { return wb.next + s * kLine; }
-__host__ __device__ __forceinline__ int32_t* ctl_live(const WfBufs& wb) { return wb.ctl; }
-__host__ __device__ __forceinline__ int32_t* ctl_list(const WfBufs& wb, int32_t par, int32_t list, int32_t s) {
-  return wb.ctl + (1 + (par * kLists + list) * 8 + s) * kLine;
+__host__ __device__ __forceinline__ int32_t* ctl_status(const WfBufs& wb) { return wb.ctl; }
+__device__ __forceinline__ int32_t* ctl_seg(const WfBufs& wb, int32_t par, int32_t s) {
+  return wb.ctl + (1 + par * kSegs + s) * kLine;
 }
-// slot-index entry k of shard s's segment of a list
+__device__ __forceinline__ int32_t* ctl_ovf(const WfBufs& wb, int32_t par) { return wb.ctl + (1 + 2 * kSegs + par) * kLine; }
+__device__ __forceinline__ int32_t* ctl_list(const WfBufs& wb, int32_t par, int32_t list, int32_t s) {
+  return wb.ctl + (3 + 2 * kSegs + (par * kLists + list) * kShards + s) * kLine;
+}
+// entry k of shard s's segment of a list
 __device__ __forceinline__ int32_t* list_slot(const WfBufs& wb, int32_t list, int32_t s, int32_t k) {
   const int32_t arr = list < kListMedium ? list : kListMedium;
-  int32_t* seg = wb.lists + (size_t)arr * (size_t)wb.capacity + (size_t)s * (size_t)wb.medseg;
+  int32_t* seg = wb.lists + ((size_t)arr * kShards + (size_t)s) * (size_t)wb.medseg;
   return list == kListNoise ? seg + wb.medseg - 1 - k : seg + k;
 }
+__device__ __forceinline__ int32_t ovf_base(const WfBufs& wb) { return kSegs * wb.seg_cap; }
+__device__ __forceinline__ int32_t fresh_base(const WfBufs& wb) { return kSegs * wb.seg_cap + wb.capacity; }
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
-
-// Slot i is processed by block (i / kWfBlock) % grid, grid a multiple of
-// kShards, so block b's slots draw chunks from shard b % kShards (blocks b and
-// b + 8 share an XCD). A 64-slot group is always one wave of wf_intersect.
-__device__ __forceinline__ int32_t slot_shard(int32_t i) { return (i / kWfBlock) % kShards; }
-
-// Wave-aggregated counter increment: this lane's ticket (meaningful only if want).
-__device__ __forceinline__ int32_t wave_ticket(bool want, int32_t* counter) {
-  unsigned long long mask = __ballot(want);
-  if (mask == 0ull) return -1;
-  int32_t prefix = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-  int32_t leader = __ffsll((long long)mask) - 1;
-  int32_t base = 0;
-  if (lane_id() == leader) base = atomicAdd(counter, (int32_t)__popcll(mask));
-  base = __shfl(base, leader);
-  return base + prefix;
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ void wave_add(bool flag, int32_t* counter, int32_t sign) {
-  unsigned long long mask = __ballot(flag);
-  if (mask && lane_id() == __ffsll((long long)mask) - 1) atomicAdd(counter, sign * (int32_t)__popcll(mask));
+// Wave-aggregated appends of the lanes of a wave to N counters (call from
+// converged code): `cls` = the lane's counter (-1: none). One ballot per
+// counter; lane k < N adds class k's lane count to counter k, so the wave's
+// appends are one atomic instruction (lanes of empty classes add nothing),
+// and each lane gets the counter's old value from its class's lane plus its
+// rank among its class's lanes. Returns the lane's slot (meaningful only for
+// cls >= 0).
+template <int N, typename Ptr>
+__device__ __forceinline__ int32_t wave_append(int32_t cls, Ptr counter_of) {
+  const int lane = lane_id();
+  unsigned long long mine = 0ull;
+  int32_t n_k = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const unsigned long long mk = __builtin_amdgcn_ballot_w64(cls == k);
+    if (cls == k) mine = mk;
+    if (lane == k) n_k = (int32_t)__popcll(mk);
+  }
+  int32_t base = 0;
+  if (lane < N && n_k > 0) base = atomicAdd(counter_of(lane), n_k);
+  base = __shfl(base, cls < 0 ? 0 : cls);
+  return base + (int32_t)lane_rank(mine);
 }
 
 // Statistics counters: each thread tallies in a register over its grid-stride
@@ -245,16 +280,22 @@ __device__ __forceinline__ void block_flush(const uint32_t (&vals)[N], void* scr
 struct Ray {
   pt_v3 o, d, thr;
   uint32_t item, ctr, meta;  // item without kFresh
-  bool fresh;                // a camera ray regenerated from its item (its slot holds only the item word)
+  bool fresh;                // a camera ray regenerated from its item (only its item word is stored)
 };
 
-// Streamed buffers (queue records, hit records, medium lists, staging) go
-// through these helpers. PMC: wf_intersect's L2 hit rate is 60 % against the
-// megakernel's 96 % (L1 hit rates 96 % / 98 %), the queue stream evicting BVH
-// lines. But the stage kernels re-read what the previous one wrote, and that
-// reuse is worth more than streaming hints: A/B on MI355X (parity-identical),
-// `nt` loads + stores / `nt` stores / `sc1` stores, C3 -10 % / -5 % / -5 %
-// (profiles/r02/ab/ab_nontemporal.log, profiles/r02/pmc_cache/).
+// A ray that continues (wf_scatter appends it to its direction's segment of
+// the next iteration's buffer; wf_drain stores it back in place).
+struct Cont {
+  pt_v3 o, d, thr;
+  uint32_t item, ctr, meta;
+  bool go;
+};
+
+// Streamed buffers (ray records, hit records, lists, staging) go through
+// these helpers. The stage kernels re-read what the previous one wrote, and
+// that reuse is worth more than streaming hints: A/B on MI355X
+// (parity-identical), `nt` loads + stores / `nt` stores / `sc1` stores, C3
+// -10 % / -5 % / -5 % (profiles/r02/ab/ab_nontemporal.log, profiles/r02/pmc_cache/).
 typedef float pt_qf4 __attribute__((ext_vector_type(4)));
 typedef float pt_qf2 __attribute__((ext_vector_type(2)));
 template <typename T>
@@ -269,36 +310,28 @@ __device__ __forceinline__ float4 q_load(const float4* p) {
   const pt_qf4 v = s_load((const pt_qf4*)p);
   return make_float4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ void q_store(float4* p, float4 v) { s_store((pt_qf4*)p, pt_qf4{v.x, v.y, v.z, v.w}); }
 __device__ __forceinline__ float2 h_load(const float2* p) {
   const pt_qf2 v = s_load((const pt_qf2*)p);
   return make_float2(v.x, v.y);
 }
 __device__ __forceinline__ void h_store(float2* p, float2 v) { s_store((pt_qf2*)p, pt_qf2{v.x, v.y}); }
 
-// A continuing ray back into its slot; a fresh ray's slot also gets its item
-// word without kFresh (the other streams were never written for it).
-__device__ __forceinline__ void store_ray_v(const Queue& q, int32_t i, pt_v3 o, pt_v3 d, pt_v3 thr, uint32_t item,
-                                            bool was_fresh, uint32_t ctr, uint32_t meta) {
-  s_store((pt_qf4*)(q.a + i), pt_qf4{o.x, o.y, o.z, d.x});
-  s_store((pt_qf2*)(q.d + i), pt_qf2{d.y, d.z});
-  s_store((pt_qf4*)(q.c + i), pt_qf4{thr.x, thr.y, thr.z, __uint_as_float(meta)});
-  s_store(q.ctr + i, ctr);
-  if (was_fresh) s_store(q.item + i, item);
+// A continuing ray's record at position p (all five streams).
+__device__ __forceinline__ void store_ray(const RayBuf& B, int32_t p, const Cont& cn) {
+  s_store((pt_qf4*)(B.a + p), pt_qf4{cn.o.x, cn.o.y, cn.o.z, cn.d.x});
+  s_store((pt_qf2*)(B.d + p), pt_qf2{cn.d.y, cn.d.z});
+  s_store((pt_qf4*)(B.c + p), pt_qf4{cn.thr.x, cn.thr.y, cn.thr.z, __uint_as_float(cn.meta)});
+  s_store(B.ctr + p, cn.ctr);
+  s_store(B.item + p, cn.item);
 }
-
-// The slot's state lives in its work-item word: an item (| kFresh), kPending or kDead.
-__device__ __forceinline__ void set_slot_item(const Queue& q, int32_t i, uint32_t v) { s_store(q.item + i, v); }
-
-__device__ __forceinline__ uint32_t slot_item(const Queue& q, int32_t i) { return s_load(q.item + i); }
 
 // Work items come in chunks of one 8x8 pixel square x csamp samples. Chunk c
 // is square c % nsq of sample block c / nsq (so early chunks cover every
 // square); item j of a chunk is pixel j % 64 of the square, sample j / 64 of
-// the block. Each 64-slot group works through one chunk at a time, so a
-// wave's rays come from one pixel square — the coherence the megakernel's
-// waves get from their 8x8 squares. Items outside the frame or past the
-// batch are skipped. it.p is the row-major pixel index (staging).
+// the block. A wave's 64 fresh rays are consecutive items, so they come
+// from one pixel square — the coherence the megakernel's waves get from
+// their 8x8 squares. Items outside the frame or past the batch are skipped.
+// it.p is the row-major pixel index (staging).
 struct Item {
   int32_t srel, p, px, py;
   bool valid;
@@ -323,37 +356,35 @@ __device__ __forceinline__ uint32_t path_key(const DevFrame& fr, const WfBufs& w
   return pt_path_key(fr.seed, (uint32_t)(it.py * fr.width + it.px), (uint32_t)(wb.s_begin + it.srel));
 }
 
-// The ray of slot i for wf_scatter, with its decoded work item. A fresh
+// The ray at position p for wf_scatter, with its decoded work item. A fresh
 // camera ray (generated and traced in this iteration's wf_intersect, not
 // stored) is regenerated from its item: the same get_ray draws
 // (kernels.py:1219-1239, direction unnormalized, Q1), throughput 1, depth and
 // wave 0.
-__device__ __forceinline__ Ray load_ray(const DevFrame& fr, const WfBufs& wb, int32_t i, Item& it) {
-  const Queue& q = wb.q;
+__device__ __forceinline__ Ray load_ray(const DevFrame& fr, const WfBufs& wb, const RayBuf& X, int32_t p, Item& it) {
   Ray r;
-  const uint32_t w = s_load(q.item + i);
+  const uint32_t w = s_load(X.item + p);
   r.fresh = (w & kFresh) != 0u;
   r.item = w & ~kFresh;
   it = decode_item(fr, wb, r.item);
   if (r.fresh) {
-    // (storing it in wf_intersect instead, 28 B, measured 1-2 % slower on C3)
+    // (storing it in wf_intersect instead, 28 B, measured 1-2 % slower on C3 in round 4)
     Rng rng{path_key(fr, wb, it), 0u};
     get_ray(fr, it.px, it.py, rng, r.o, r.d);
     r.ctr = rng.n;
     r.thr = pt_v3f(1.0f, 1.0f, 1.0f);
     r.meta = 0u;
   } else {
-    const float4 a = q_load(q.a + i), c = q_load(q.c + i);
-    const float2 d = h_load(q.d + i);
+    const float4 a = q_load(X.a + p), c = q_load(X.c + p);
+    const float2 d = h_load(X.d + p);
     r.o = pt_v3f(a.x, a.y, a.z);
     r.d = pt_v3f(a.w, d.x, d.y);
-    r.ctr = s_load(q.ctr + i);
+    r.ctr = s_load(X.ctr + p);
     r.thr = pt_v3f(c.x, c.y, c.z);
     r.meta = __float_as_uint(c.w);
   }
   return r;
 }
-
 
 __device__ __forceinline__ void stage(const DevFrame& fr, const WfBufs& wb, uint32_t k, pt_v3 c) {
   const Item it = decode_item(fr, wb, k);
@@ -363,116 +394,160 @@ __device__ __forceinline__ void stage(const DevFrame& fr, const WfBufs& wb, uint
   s_store(p + 2, c.z);
 }
 
+// ------------------------------------------------------------ work pool
 __device__ __forceinline__ int32_t shard_end(const WfBufs& wb, int32_t s) {
   int64_t e = (int64_t)(s + 1) * wb.shard_len;
-  return e < wb.nunits ? (int32_t)e : wb.nunits;
+  return e < wb.nitems ? (int32_t)e : wb.nitems;
 }
 
-// Next units for a group of shard `shard` (one lane calls it), stealing from
-// the other shards once its own range is spent: {first, end} unit, or
-// first = -1 when the batch is done. A whole chunk (csamp units of one
-// square) while the shard has plenty left; single units in its tail, so no
-// group is left with a long private queue while the others retire.
-__device__ __forceinline__ int2 fetch_units(const WfBufs& wb, int32_t shard) {
-  for (int32_t a = 0; a < kShards; ++a) {
-    const int32_t s = (shard + a) % kShards;
+// True when every pool shard is spent (wave-uniform; lane s < kShards reads
+// shard s). Counters only grow, so a stale read can only say "not empty".
+// wf_scatter looks once per iteration, after all of the iteration's claims;
+// the next wf_intersect then claims in none of its waves or may claim in all.
+__device__ __forceinline__ bool pool_dry(const WfBufs& wb) {
+  const int lane = lane_id();
+  bool left = false;
+  if (lane < kShards)
+    left = __hip_atomic_load(ctl_next(wb, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shard_end(wb, lane);
+  return pt_ballot(left) == 0ull;
+}
+
+// Work items for the lanes of a wave that want one (call from converged
+// code): consecutive items of the wave's own shard, one atomic per wave and
+// shard tried, then of the other shards while lanes are left; -1 for a lane
+// that gets none (the pool is empty). A counter may run past its shard's end
+// (by at most the lanes asking at once): it only grows.
+__device__ __forceinline__ int32_t claim_items(const WfBufs& wb, int32_t shard, bool want) {
+  const unsigned long long m = pt_ballot(want);
+  if (m == 0ull) return -1;
+  const int32_t n = (int32_t)__popcll(m), rank = (int32_t)lane_rank(m);
+  int32_t item = -1, taken = 0;
+  for (int32_t a = 0; a < kShards && taken < n; ++a) {
+    const int32_t s = (shard + a) & (kShards - 1);
     const int32_t e = shard_end(wb, s);
-    const int32_t cur = __hip_atomic_load(ctl_next(wb, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur >= e) continue;
-    const int32_t take = (e - cur) >= PTMI_WF_TAIL * wb.shard_groups * wb.csamp ? wb.csamp : 1;
-    const int32_t t = atomicAdd(ctl_next(wb, s), take);
-    if (t < e) return make_int2(t, t + take < e ? t + take : e);
-  }
-  return make_int2(-1, -1);
-}
-
-// Initial state: every slot waits for work; groups own no units yet; shard s
-// starts at its first unit.
-__global__ __launch_bounds__(kWfBlock) void wf_generate(DevFrame fr, WfBufs wb, int32_t init_next) {
-  for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity; i += (int32_t)(gridDim.x * kWfBlock)) {
-    wb.q.item[i] = kPending;
-    if ((i & 63) == 0) wb.grp[i >> 6] = make_int2(0, 0);
-  }
-  if (init_next && blockIdx.x < kShards && threadIdx.x == 0) {
-    const int32_t s = (int32_t)blockIdx.x;
-    *ctl_next(wb, s) = min(s * wb.shard_len, wb.nunits);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ctl_live(wb) = wb.capacity;
-}
-
-// Hand the group's (this wave's) next items to its slots waiting for work,
-// taking a new chunk when the current one runs out; slots that find no work
-// retire. Wave-uniform: called by all 64 lanes of the group. A slot given a
-// camera ray gets its origin and direction in (o, d) (true returned); only
-// its item word is stored, marked kFresh (wf_scatter regenerates the ray).
-__device__ __forceinline__ bool assign_work(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& item,
-                                            pt_v3& o, pt_v3& d) {
-  const bool pending = item == kPending;
-  const unsigned long long pm = __ballot(pending);
-  if (pm == 0ull) return false;
-  const int32_t g = i >> 6;
-  const uint32_t n = (uint32_t)__popcll(pm);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
-  const int2 gs = wb.grp[g];
-  uint32_t nxt = (uint32_t)gs.x, end = (uint32_t)gs.y;
-  const uint32_t avail = end - nxt;
-  uint32_t my = kDead;
-  if (rank < avail) my = nxt + rank;
-  if (n > avail) {  // the group needs new units (>= 64 items: one fetch is enough)
-    int2 u = make_int2(0, 0);
-    const int32_t leader = __ffsll((long long)pm) - 1;
-    if (lane_id() == leader) u = fetch_units(wb, slot_shard(i));
-    u.x = __shfl(u.x, leader);
-    u.y = __shfl(u.y, leader);
-    if (u.x >= 0) {
-      const uint32_t cb = 64u * (uint32_t)u.x;
-      if (rank >= avail) my = cb + (rank - avail);
-      nxt = cb + (n - avail);
-      end = 64u * (uint32_t)u.y;
-    } else {
-      nxt = end;
+    int32_t t = e;
+    if (lane_id() == 0) {
+      t = __hip_atomic_load(ctl_next(wb, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t < e) t = atomicAdd(ctl_next(wb, s), n - taken);
     }
-  } else {
-    nxt += n;
+    t = __shfl(t, 0);
+    const int32_t got = t < e ? (e - t < n - taken ? e - t : n - taken) : 0;
+    if (want && rank >= taken && rank < taken + got) item = t + (rank - taken);
+    taken += got;
   }
-  if (lane_id() == 0) wb.grp[g] = make_int2((int32_t)nxt, (int32_t)end);
-  bool fresh = false;
-  if (pending) {
-    if (my == kDead) {
-      set_slot_item(wb.q, i, kDead);
-      item = kDead;
-    } else if (decode_item(fr, wb, my).valid) {
-      // generate_camera_rays, kernels.py:1219-1239 (direction left unnormalized, Q1)
-      const Item it = decode_item(fr, wb, my);
-      Rng rng{path_key(fr, wb, it), 0u};
-      get_ray(fr, it.px, it.py, rng, o, d);
-      item = my | kFresh;
-      set_slot_item(wb.q, i, item);
-      fresh = true;
-    }  // an item outside the frame / batch: the slot stays pending
-  }
-  wave_add(pending && my == kDead, ctl_live(wb), -1);
-  return fresh;
+  return item;
 }
 
-// Path end without a scatter (a miss, or an emissive / absorbing hit): its
-// one colour (or 0) to the staging slot, and the slot waits for work.
-__device__ __forceinline__ void end_path(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t item, pt_v3 c) {
-  stage(fr, wb, item, c);
-  set_slot_item(wb.q, i, kPending);
+// Initial state of a batch (the host zeroed every counter): pool shard s
+// starts at its first item.
+__global__ __launch_bounds__(64) void wf_generate(WfBufs wb) {
+  const int32_t s = (int32_t)threadIdx.x;
+  if (s < kShards) *ctl_next(wb, s) = min(s * wb.shard_len, wb.nitems);
+}
+
+// ------------------------------------------------------------ segments
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t t = __shfl_up(v, (unsigned)o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// The continuing rays of one parity, as a wave sees them: lane l < kSegs
+// holds the entries of the lower shards' segments of its bin; lane b <
+// kBins its bin's first work index and size. Work indices: the bins in
+// order, each padded to whole waves, then the overflow region, padded, then
+// the fresh rays. A segment's counter counts every append; its region holds
+// seg_cap (the rest went to the overflow region).
+struct SegTable {
+  int32_t pre, bstart, btot;                    // per lane (see above)
+  int32_t ovf_start, ovf_n, fresh_start, live;  // wave-uniform; live = continuing rays
+};
+__device__ __forceinline__ SegTable seg_table(const WfBufs& wb, int32_t par) {
+  SegTable T;
+  const int lane = lane_id();
+  const int32_t c = lane < kSegs ? min(s_load(ctl_seg(wb, par, lane)), wb.seg_cap) : 0;
+  const int32_t incl = wave_incl_scan(c);
+  const int32_t first = lane & ~(kShards - 1);
+  const int32_t below = __shfl(incl, first > 0 ? first - 1 : 0);
+  T.pre = incl - c - (first > 0 ? below : 0);
+  const int32_t bl = lane < kBins ? lane : 0;
+  const int32_t hi = __shfl(incl, bl * kShards + kShards - 1);
+  const int32_t lo = __shfl(incl, bl > 0 ? bl * kShards - 1 : 0);
+  T.btot = lane < kBins ? hi - (bl > 0 ? lo : 0) : 0;
+  const int32_t span = (T.btot + 63) & ~63;
+  const int32_t sincl = wave_incl_scan(span);
+  T.bstart = sincl - span;
+  const int32_t spans = __shfl(sincl, 63);
+  const int32_t ov = __builtin_amdgcn_readfirstlane(min(s_load(ctl_ovf(wb, par)), wb.capacity));
+  T.ovf_start = spans;
+  T.ovf_n = ov;
+  T.fresh_start = spans + ((ov + 63) & ~63);
+  T.live = __shfl(incl, 63) + ov;
+  return T;
+}
+
+// Position of work index w0 + lane (w0 a wave's base, below fresh_start), or
+// -1 for a padding lane.
+__device__ __forceinline__ int32_t cont_position(const SegTable& T, const WfBufs& wb, int32_t w0) {
+  const int lane = lane_id();
+  if (w0 >= T.ovf_start) {
+    const int32_t j = w0 - T.ovf_start + lane;
+    return j < T.ovf_n ? ovf_base(wb) + j : -1;
+  }
+  const unsigned long long m = pt_ballot(lane < kBins && T.bstart <= w0 && w0 < T.bstart + T.btot);
+  const int32_t b = __ffsll((long long)m) - 1;  // wave-uniform: the bin this wave reads
+  const int32_t j = w0 - __builtin_amdgcn_readlane(T.bstart, b) + lane;
+  if (j >= __builtin_amdgcn_readlane(T.btot, b)) return -1;
+  int32_t s = 0, off = j;
+#pragma unroll
+  for (int k = 1; k < kShards; ++k) {
+    const int32_t pk = __builtin_amdgcn_readlane(T.pre, b * kShards + k);
+    if (j >= pk) {
+      s = k;
+      off = j - pk;
+    }
+  }
+  return (b * kShards + s) * wb.seg_cap + off;
+}
+
+// Direction bin of a continuing ray: its octant.
+__device__ __forceinline__ int32_t ray_bin(pt_v3 d) {
+  if constexpr (kBins == 1) {
+    return 0;
+  } else {
+    return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
+  }
+}
+
+// Appends the wave's continuing rays to their segments of the next
+// iteration's buffer (call from converged code): one atomic per wave and
+// non-empty bin (one instruction, wave_append), then each ray's record to
+// its position; ranks past a segment's region go to the overflow region
+// (one more atomic).
+__device__ __forceinline__ void append_cont(const WfBufs& wb, int32_t npar, int32_t shard, const Cont& cn) {
+  const RayBuf& Y = wb.rb[npar];
+  const int32_t bin = cn.go ? ray_bin(cn.d) : -1;
+  const int32_t k = wave_append<kBins>(bin, [&](int32_t b) { return ctl_seg(wb, npar, b * kShards + shard); });
+  const bool over = cn.go && k >= wb.seg_cap;
+  const int32_t o = wave_append<1>(over ? 0 : -1, [&](int32_t) { return ctl_ovf(wb, npar); });
+  if (cn.go) store_ray(Y, over ? ovf_base(wb) + o : (bin * kShards + shard) * wb.seg_cap + k, cn);
 }
 
 // A path that ends without a scatter (its traced segment has class
 // kListEnded): a miss adds thr * background (shade_miss_rays, kernels.py:
 // 1266-1280), an emissive hit thr * emit when the emit colour is non-zero
-// (kernels.py:1365-1375). w = the slot's item word (a fresh camera ray's
+// (kernels.py:1365-1375). w = the ray's item word (a fresh camera ray's
 // throughput is 1: no C record was stored for it), ref = the hit's leaf code,
-// 0 for a miss.
-__device__ __forceinline__ void end_unscattered(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t i,
-                                                uint32_t w, int32_t ref) {
+// 0 for a miss. Its one colour goes to the staging slot.
+__device__ __forceinline__ void end_unscattered(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
+                                                const RayBuf& X, int32_t p, uint32_t w, int32_t ref) {
   pt_v3 thr = pt_v3f(1.0f, 1.0f, 1.0f);
   if (!(w & kFresh)) {
-    const float4 c = q_load(wb.q.c + i);
+    const float4 c = q_load(X.c + p);
     thr = pt_v3f(c.x, c.y, c.z);
   }
   pt_v3 col = pt_mul(thr, pt_v3f(fr.bg[0], fr.bg[1], fr.bg[2]));
@@ -480,7 +555,7 @@ __device__ __forceinline__ void end_unscattered(const DevScene& sc, const DevFra
     const float4 e = sc.mats[5 * mat_index(sc, ref) + 1];  // emit colour (Mat::m1)
     col = (e.x > 0.0f || e.y > 0.0f || e.z > 0.0f) ? pt_mul(thr, pt_v3f(e.x, e.y, e.z)) : pt_v3f(0.0f, 0.0f, 0.0f);
   }
-  end_path(fr, wb, i, w & ~kFresh, col);
+  stage(fr, wb, w & ~kFresh, col);
 }
 
 // Closest-hit classes (PTMI_CLASS_*, include/ptmi.h) are packed into the
@@ -494,13 +569,23 @@ static_assert(PTMI_CLASS_LAMBERTIAN == kListLambertian && PTMI_CLASS_GLOSSY == k
                   PTMI_CLASS_NOISE == kListNoise && PTMI_CLASS_EMISSIVE == kListEnded,
               "leaf classes are list ids");
 
+// Appends position p to the list of class `list` (-1: none) of this
+// iteration, one atomic per wave and non-empty list (one instruction,
+// wave_append; call from converged code).
+__device__ __forceinline__ void append_list(const WfBufs& wb, int32_t par, int32_t shard, int32_t list, int32_t p) {
+  const int32_t k = wave_append<kLists>(list, [&](int32_t l) { return ctl_list(wb, par, l, shard); });
+  if (list >= 0 && k < wb.medseg) s_store(list_slot(wb, list, shard, k), p);  // always < medseg: it bounds a shard's rays
+}
+
 // intersect_rays, kernels.py:1242-1263, plus the closest-hit classification:
 // a miss (shade_miss_rays, kernels.py:1266-1280) or an emissive hit
-// (kernels.py:1365-1375) ends its path here; every other traced slot is
-// appended to the list of its hit's material class. Its streams: the item
-// word of every slot, o and d of a traced one (24 B), the hit record (8 B)
-// and one list entry (4 B); a path end reads thr (16 B) and writes its
-// staging slot and item word. A fresh camera ray is not stored.
+// (kernels.py:1365-1375) ends its path here; every other traced ray is
+// appended to the list of its hit's material class. The work: this
+// iteration's continuing rays, segment by segment (each wave reads 64 rays of
+// one direction bin, coalesced: item word + o, d = 28 B per ray), then the
+// fresh camera rays that fill the pipe back up to `capacity` while the pool
+// lasts. Writes the hit record (8 B) and one list entry (4 B) per ray; a path
+// end reads thr (16 B) and writes its staging slot.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
@@ -508,68 +593,65 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
   __shared__ uint2 lds_stack[LDS * kWfBlock];
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid, wb.spill, (uint32_t)(blockIdx.x * kWfBlock + tid) * 8u, gridDim.x * kWfBlock * 8u};
-  const Queue q = wb.q;
+  const RayBuf& X = wb.rb[par];
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
+  const SegTable T = seg_table(wb, par);
+  // the pool was empty once the previous iteration's claims were done (the
+  // previous wf_scatter looked): then this launch claims nothing, in every
+  // wave, and traces exactly the continuing rays
+  const bool dry = __builtin_amdgcn_readfirstlane(s_load(ctl_status(wb) + 2)) != 0;
+  const int32_t nfresh = dry ? 0 : max(wb.capacity - T.live, 0);
+  const int32_t nwork = T.fresh_start + nfresh;
+  if (blockIdx.x == 0 && tid == 0) {  // for the host: the rays this launch traces when the pool was empty
+    ctl_status(wb)[0] = T.live;
+    ctl_status(wb)[1] = dry ? 1 : 0;
+  }
   uint32_t n_live = 0, n_ended = 0;
-  for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + tid); i < wb.capacity; i += stride) {
-    uint32_t item = s_load(q.item + i);
+  for (int32_t w0 = (int32_t)(blockIdx.x * kWfBlock) + (tid & ~63); w0 < nwork; w0 += stride) {
+    int32_t p = -1;
+    uint32_t item = 0u;
     pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
-    // generate_camera_rays (kernels.py:1219-1239) for slots that need work
-    const bool fresh = assign_work(fr, wb, i, item, o, d);
-    int32_t list = -1;
-    if (item < kPending) {
-      ++n_live;
-      if (!fresh) {
-        const float4 a = q_load(q.a + i);
-        const float2 dyz = h_load(q.d + i);
+    if (w0 < T.fresh_start) {  // a continuing ray of a segment or of the overflow region
+      p = cont_position(T, wb, w0);
+      if (p >= 0) {
+        item = s_load(X.item + p);
+        const float4 a = q_load(X.a + p);
+        const float2 dyz = h_load(X.d + p);
         o = pt_v3f(a.x, a.y, a.z);
         d = pt_v3f(a.w, dyz.x, dyz.y);
       }
+    } else {  // generate_camera_rays (kernels.py:1219-1239) for the next work items
+      const int32_t f = w0 - T.fresh_start + lane_id();
+      const int32_t k = claim_items(wb, shard, f < nfresh);
+      if (k >= 0) {
+        const Item it = decode_item(fr, wb, (uint32_t)k);
+        if (it.valid) {  // (padding items of squares past the frame / batch are skipped)
+          Rng rng{path_key(fr, wb, it), 0u};
+          get_ray(fr, it.px, it.py, rng, o, d);  // direction left unnormalized (Q1)
+          p = fresh_base(wb) + f;
+          item = (uint32_t)k | kFresh;
+          s_store(X.item + p, item);
+        }
+      }
+    }
+    int32_t list = -1;
+    if (p >= 0) {
+      ++n_live;
       float t = 0.0f;
       int32_t ref = 0;
       const bool hit = traverse<STACK, kWfBlock, TRAV, LDS>(sc, o, d, kTMin, kTMax, st, t, ref);
       if (!hit) ref = 0;  // a miss: no leaf code
       list = hit ? leaf_class(ref) : kListEnded;
       if (list == kListEnded) {
-        end_unscattered(sc, fr, wb, i, item, ref);
+        end_unscattered(sc, fr, wb, X, p, item, ref);
         ++n_ended;
         list = -1;
       } else {
-        h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
+        h_store(X.hit + p, make_float2(t, __int_as_float(ref)));
       }
     }
-    // wave-uniform appends, one atomic per wave and non-empty list; lane 0
-    // issues them all before it waits for any (independent round trips)
-    unsigned long long m[kLists];
-    int32_t got[kLists];
-#pragma unroll
-    for (int32_t l = 0; l < kLists; ++l) {
-      m[l] = pt_ballot(list == l);
-      got[l] = 0;
-    }
-    if (lane_id() == 0) {
-#pragma unroll
-      for (int32_t l = 0; l < kLists; ++l)
-        if (m[l]) got[l] = atomicAdd(ctl_list(wb, par, l, shard), (int32_t)__popcll(m[l]));
-    }
-    // broadcast lane 0's bases: in converged code (every lane of the wave
-    // active here), so that lane 0 takes part whatever its own list
-    int32_t b0 = 0;
-    unsigned long long ml = 0ull;
-#pragma unroll
-    for (int32_t l = 0; l < kLists; ++l) {
-      const int32_t bl = __shfl(got[l], 0);
-      if (list == l) {
-        b0 = bl;
-        ml = m[l];
-      }
-    }
-    if (list >= 0) {
-      const int32_t k = b0 + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
-      if (k < wb.medseg) s_store(list_slot(wb, list, shard, k), i);  // always true: a shard has medseg slots
-    }
+    append_list(wb, par, shard, list, p);
   }
   if (counters) {
     block_flush<1>({n_live}, lds_stack, counters + 0);
@@ -578,12 +660,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
 }
 
 // scatter epilogue of shade_and_scatter (kernels.py:1377-1399) plus the
-// per-path wave budget of renderer.py:313: a continuing ray is stored back
-// into its slot i (true returned). A path it ends is counted in ends[0]
-// (Russian roulette) or ends[1] (depth or wave budget).
-__device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, const WfBufs& wb, int32_t i, bool scattered,
-                                                 pt_v3 hp, pt_v3 sdir, pt_v3 att, const Ray& cur, Rng& r,
-                                                 uint32_t (&ends)[2]) {
+// per-path wave budget of renderer.py:313: a continuing ray goes to cn (true
+// returned). A path it ends is counted in ends[0] (Russian roulette) or
+// ends[1] (depth or wave budget).
+__device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, bool scattered, pt_v3 hp, pt_v3 sdir,
+                                                 pt_v3 att, const Ray& cur, Rng& r, uint32_t (&ends)[2], Cont& cn) {
   if (!scattered) return false;
   pt_v3 nthr = pt_mul(cur.thr, att);
   int32_t nd = (int32_t)(cur.meta & 0xffu) + 1;
@@ -604,18 +685,22 @@ __device__ __forceinline__ bool scatter_epilogue(const DevFrame& fr, const WfBuf
     ++ends[1];
     return false;
   }
-  store_ray_v(wb.q, i, hp, sdir, nthr, cur.item, cur.fresh, r.n, (uint32_t)nd | ((uint32_t)(wave + 1) << 8));
+  cn.o = hp;
+  cn.d = sdir;
+  cn.thr = nthr;
+  cn.item = cur.item;
+  cn.ctr = r.n;
+  cn.meta = (uint32_t)nd | ((uint32_t)(wave + 1) << 8);
+  cn.go = true;
   return true;
 }
 
-// Per-lane tail of wf_scatter for a path a scatter ended: stage its colour
-// (0 unless it ended on an emissive boundary fallback; misses and emissive
-// surface hits end in wf_intersect, end_unscattered) and mark the slot as
-// waiting for work (the next wf_intersect hands it the next item).
-__device__ __forceinline__ void finish_ended(const DevFrame& fr, const WfBufs& wb, int32_t i, const Ray& ray,
-                                             pt_v3 emit) {
-  end_path(fr, wb, i, ray.item,
-           (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit) : pt_v3f(0.0f, 0.0f, 0.0f));
+// Per-lane tail of a path a scatter ended: stage its colour (0 unless it
+// ended on an emissive boundary fallback; misses and emissive surface hits
+// end in wf_intersect, end_unscattered).
+__device__ __forceinline__ void finish_ended(const DevFrame& fr, const WfBufs& wb, const Ray& ray, pt_v3 emit) {
+  stage(fr, wb, ray.item,
+        (emit.x > 0.0f || emit.y > 0.0f || emit.z > 0.0f) ? pt_mul(ray.thr, emit) : pt_v3f(0.0f, 0.0f, 0.0f));
 }
 
 // Shard s and offset of entry j of a list whose shard segments hold cnt[s]
@@ -642,15 +727,16 @@ __device__ __forceinline__ int32_t list_counts(const WfBufs& wb, int32_t par, in
   return n;
 }
 
-
-// One entry i of the Lambertian, glossy or dielectric list (`list`,
-// wave-uniform): shade_and_scatter for a surface hit (kernels.py:1359-1399).
-__device__ __forceinline__ void shade_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, int32_t list,
-                                            int32_t i, uint32_t& n_ended, uint32_t (&ends)[2]) {
-  const float2 h = h_load(wb.hit + i);
+// The ray at position p of the Lambertian, glossy or dielectric list
+// (`list`, wave-uniform): shade_and_scatter for a surface hit
+// (kernels.py:1359-1399). A continuing ray goes to cn.
+__device__ __forceinline__ void shade_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
+                                            const RayBuf& X, int32_t list, int32_t p, uint32_t& n_ended,
+                                            uint32_t (&ends)[2], Cont& cn) {
+  const float2 h = h_load(X.hit + p);
   const int32_t ref = __float_as_int(h.y);
   Item it;
-  const Ray ray = load_ray(fr, wb, i, it);
+  const Ray ray = load_ray(fr, wb, X, p, it);
   const Mat m = load_mat(sc, mat_index(sc, ref));
   Rng r{path_key(fr, wb, it), ray.ctr};
   const pt_v3 hp = pt_add(ray.o, pt_scale(ray.d, h.x));
@@ -665,25 +751,26 @@ __device__ __forceinline__ void shade_entry(const DevScene& sc, const DevFrame& 
   } else {
     sc_ok = scatter(sc, ref, m, ray.d, hp, nrm, r, sdir, att);
   }
-  const bool go = scatter_epilogue(fr, wb, i, sc_ok, hp, sdir, att, ray, r, ends);
-  if (!go) {
-    finish_ended(fr, wb, i, ray, emitted(m));
+  if (!scatter_epilogue(fr, sc_ok, hp, sdir, att, ray, r, ends, cn)) {
+    finish_ended(fr, wb, ray, emitted(m));
     ++n_ended;
   }
 }
 
-// One entry i of the constant-medium list (exit traversal + free flight,
-// apply_constant_medium kernels.py:365-450, and the volume branch of
+// The ray at position p of the constant-medium list (exit traversal + free
+// flight, apply_constant_medium kernels.py:365-450, and the volume branch of
 // shade_and_scatter, kernels.py:1326-1357) or, is_noise, of the Perlin list.
+// A continuing ray (a scatter, or a passthrough at the same depth) goes to cn.
 template <int STACK, int TRAV>
 __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, Stack st,
-                                             int32_t i, bool is_noise, uint32_t& n_ended, uint32_t (&ends)[2]) {
-  bool ended = false, go = false;
+                                             const RayBuf& X, int32_t p, bool is_noise, uint32_t& n_ended,
+                                             uint32_t (&ends)[2], Cont& cn) {
+  bool go = false;
   pt_v3 emit = pt_v3f(0.0f, 0.0f, 0.0f);
-  const float2 h = h_load(wb.hit + i);
+  const float2 h = h_load(X.hit + p);
   const int32_t ref = __float_as_int(h.y);
   Item it;
-  const Ray ray = load_ray(fr, wb, i, it);
+  const Ray ray = load_ray(fr, wb, X, p, it);
   float te = 0.0f;
   int32_t rex = 0;
   bool hx = false;
@@ -709,8 +796,13 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
         ++ends[1];  // Q14: no wave left for the passthrough
       } else {
         float eps_t = 0.001f / sqrtf(pt_dot(ray.d, ray.d));
-        store_ray_v(wb.q, i, pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t)), ray.d, ray.thr, ray.item, ray.fresh,
-                    r.n, ray.meta + (1u << 8));
+        cn.o = pt_add(ray.o, pt_scale(ray.d, t_exit + eps_t));
+        cn.d = ray.d;
+        cn.thr = ray.thr;
+        cn.item = ray.item;
+        cn.ctr = r.n;
+        cn.meta = ray.meta + (1u << 8);
+        cn.go = true;
         go = true;
       }
     } else {  // fallback: the boundary as a surface (kernels.py:1352-1357)
@@ -728,10 +820,11 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
     if (ruv == kRuvMedium) sdir = v;
     else scattered = scatter_end(sc, ruv, ref, m, hp, nrm, v, sdir, att);
   }
-  if (!passthrough) go = scatter_epilogue(fr, wb, i, scattered, hp, sdir, att, ray, r, ends);
-  ended = !go;
-  if (ended) finish_ended(fr, wb, i, ray, emit);
-  n_ended += ended ? 1u : 0u;
+  if (!passthrough) go = scatter_epilogue(fr, scattered, hp, sdir, att, ray, r, ends, cn);
+  if (!go) {
+    finish_ended(fr, wb, ray, emit);
+    ++n_ended;
+  }
 }
 
 // shade_and_scatter (kernels.py:1289-1399) and the constant-medium exit
@@ -747,12 +840,16 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
 // +4.8 %, mesh fog -1.8 % (the shading waves run at the medium's 4
 // waves/SIMD; profiles/r03/ab/ab_wf_fused.log). The surface hit point and
 // normal are the reference's (kernels.py:1359-1364); every draw keeps the
-// reference's order.
+// reference's order. The continuing rays go to their direction segments of
+// the next iteration's buffer (append_cont).
 #ifndef PTMI_WF_SCATTER_MIN_WAVES
-// 5 waves/SIMD: <= 96 VGPRs (the 16-slot kernel: 96, 72 B/lane of scratch, against 116 VGPRs and 52 B at 4
-// waves). A/B on MI355X, parity-identical: C3 +2.1 %, mesh fog +3 % (profiles/r03/ab/ab_wf_scatter_waves.log).
-// Kernels of more than 16 stack slots stay at 4 (their 20+ KB LDS stacks allow no more).
-#define PTMI_WF_SCATTER_MIN_WAVES 5
+// 4 waves/SIMD: <= 128 VGPRs. Round 3 measured 5 waves (96 VGPRs, 72 B/lane
+// of scratch) +2.1 % on C3; since the continuing rays are appended by the
+// wave (round 5) the 5-wave build spills 148 B/lane (24 scratch stores in the
+// loop) and the 4-wave build 52 B: A/B on MI355X, parity-identical, 4 waves
+// C3 +2.2 % (1914-1923 vs 1856-1899), mesh fog +3 % (profiles/r05/ab/ab_wf_sort.log).
+// Kernels of more than 16 stack slots: their 20+ KB LDS stacks allow no more.
+#define PTMI_WF_SCATTER_MIN_WAVES 4
 #endif
 // The medium waves' LDS stacks cap this kernel at 5 waves/SIMD. A/B on
 // MI355X (round 4): split into a medium launch (5 waves) and a launch for the
@@ -765,6 +862,8 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
+  const RayBuf& X = wb.rb[par];
+  const int32_t shard = (int32_t)(blockIdx.x % kShards);
   int32_t cnt[kLists][kShards], num[kLists], span[kLists];  // wave-uniform
   int32_t n = 0;
 #pragma unroll
@@ -775,115 +874,100 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
   }
   if (blockIdx.x < kShards && threadIdx.x < kLists)  // the next iteration's lists start empty
     *ctl_list(wb, par ^ 1, (int32_t)threadIdx.x, (int32_t)blockIdx.x) = 0;
+  // this iteration's segments were read by its wf_intersect: they start empty
+  // for the next wf_scatter's appends (which go to this parity)
+  if (blockIdx.x == 0 && threadIdx.x < kSegs) *ctl_seg(wb, par, (int32_t)threadIdx.x) = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctl_ovf(wb, par) = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters && num[0] > 0)
     atomicAdd(counters + 1, (unsigned long long)num[0]);  // medium exit traversals
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // every claim of this iteration is done: is the pool empty?
+    const bool d = pool_dry(wb);
+    if (threadIdx.x == 0) ctl_status(wb)[2] = d ? 1 : 0;
+  }
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock); base < n; base += stride) {
+  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock) + (int32_t)(threadIdx.x & ~63u); base < n; base += stride) {
     // wave-uniform list of this wave's 64 entries
-    int32_t j = base + (int32_t)threadIdx.x, l = 0;
+    int32_t j = base + lane_id(), l = 0;
 #pragma unroll
     for (int k = 0; k + 1 < kLists; ++k)
       if (l == k && j >= span[k]) {
         j -= span[k];
         l = k + 1;
       }
-    int32_t i = -1;
+    int32_t p = -1;
 #pragma unroll
     for (int k = 0; k < kLists; ++k)
-      if (l == k && j < num[k]) i = list_entry(wb, kScatterOrder[k], cnt[k], j);
-    if (i < 0) continue;  // the list's padding
+      if (l == k && j < num[k]) p = list_entry(wb, kScatterOrder[k], cnt[k], j);
     int32_t lid = kScatterOrder[0];  // this wave's list (wave-uniform select, no indexed table)
 #pragma unroll
     for (int k = 1; k < kLists; ++k)
       if (l == k) lid = kScatterOrder[k];
-    if (lid == kListMedium || lid == kListNoise) medium_entry<STACK, TRAV>(sc, fr, wb, st, i, lid == kListNoise, n_ended, ends);
-    else shade_entry(sc, fr, wb, lid, i, n_ended, ends);
+    Cont cn;
+    cn.go = false;
+    if (p >= 0) {  // (p < 0: the list's padding)
+      if (lid == kListMedium || lid == kListNoise)
+        medium_entry<STACK, TRAV>(sc, fr, wb, st, X, p, lid == kListNoise, n_ended, ends, cn);
+      else
+        shade_entry(sc, fr, wb, X, lid, p, n_ended, ends, cn);
+    }
+    append_cont(wb, par ^ 1, shard, cn);
   }
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
 }
 
-// The tail of a batch (wf_batch switches a pipe to it once its live slots fall
-// below 1 / drain_at of its capacity, i.e. after the work pool ran dry: a
-// slot retires only when fetch_units finds every shard empty): one launch
-// finishes every path still in the pipe, each lane looping intersect ->
-// classify -> shade over its own slot until the path ends — exactly the
-// per-path steps of wf_intersect and wf_scatter (the same entry functions,
-// reading and writing the same slot), so every path, its draws, its wave
-// budget (Q14) and the counters are unchanged. The shards are empty, but a
-// group may still hold items it fetched and has not handed out yet
-// (wb.grp[g]: up to 63 of a single tail unit, more after a whole-chunk
-// fetch): a lane whose slot waits for work, or whose path ends, claims the
-// group's next item with an atomic on wb.grp[g].x and traces its camera ray
-// (generate_camera_rays, kernels.py:1219-1239) in the same loop, until the
-// group's range is spent. What changes is the schedule: instead of one
-// intersect and one scatter launch per remaining wave (~7.5 us each even when
-// nearly empty, and ~50 of them for the longest Russian-roulette survivors),
-// the tail is one launch whose length is the longest remaining chain of
-// paths of one slot. Launched on the pipe's stream after a wf_scatter, so no
-// slot is fresh and the lists are not used.
-__device__ __forceinline__ bool drain_claim(const DevFrame& fr, const WfBufs& wb, int32_t i, uint32_t& w, pt_v3& o,
-                                            pt_v3& d) {
-  int32_t* const nxt = &wb.grp[i >> 6].x;
-  const int32_t end = wb.grp[i >> 6].y;  // not changed by this launch
-  for (;;) {
-    const int32_t k = atomicAdd(nxt, 1);
-    if (k >= end) {
-      set_slot_item(wb.q, i, kDead);
-      return false;
-    }
-    const Item it = decode_item(fr, wb, (uint32_t)k);
-    if (!it.valid) continue;  // padding of a square outside the frame / past the batch
-    Rng rng{path_key(fr, wb, it), 0u};
-    get_ray(fr, it.px, it.py, rng, o, d);
-    w = (uint32_t)k | kFresh;  // wf_scatter's entry functions regenerate the ray from it (load_ray)
-    set_slot_item(wb.q, i, w);
-    return true;
-  }
-}
-
+// The tail of a batch (wf_batch switches a pipe to it once the work pool is
+// empty and the pipe traces fewer than capacity / drain_at rays per
+// iteration): one launch finishes every path still in the pipe, each lane
+// looping intersect -> classify -> shade over its own ray until the path
+// ends — exactly the per-path steps of wf_intersect and wf_scatter (the same
+// entry functions), with the continuing ray stored back in place, so every
+// path, its draws, its wave budget (Q14) and the counters are unchanged.
+// What changes is the schedule: instead of one intersect and one scatter
+// launch per remaining wave (~7.5 us each even when nearly empty, and ~50 of
+// them for the longest Russian-roulette survivors), the tail is one launch
+// whose length is the longest remaining path. Launched on the pipe's stream
+// after a wf_scatter, on the continuing rays of the next iteration's parity:
+// the pool is empty, so no fresh ray is due.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-__global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                    unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
-  const Queue q = wb.q;
+  const RayBuf& X = wb.rb[par];
+  const SegTable T = seg_table(wb, par);
   uint32_t n_seg = 0, n_med = 0, n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t i = (int32_t)(blockIdx.x * kWfBlock + threadIdx.x); i < wb.capacity;
-       i += (int32_t)(gridDim.x * kWfBlock)) {
-    uint32_t w = s_load(q.item + i);
-    if (w == kDead) continue;  // retired: its group's items are all handed out
+  for (int32_t w0 = (int32_t)(blockIdx.x * kWfBlock) + (int32_t)(threadIdx.x & ~63u); w0 < T.fresh_start;
+       w0 += (int32_t)(gridDim.x * kWfBlock)) {
+    const int32_t p = cont_position(T, wb, w0);
+    if (p < 0) continue;
     for (;;) {
-      pt_v3 o, d;
-      if (w == kPending) {  // waiting for work: the group's next item, if any
-        if (!drain_claim(fr, wb, i, w, o, d)) break;
-      } else {
-        const float4 a = q_load(q.a + i);
-        const float2 dyz = h_load(q.d + i);
-        o = pt_v3f(a.x, a.y, a.z);
-        d = pt_v3f(a.w, dyz.x, dyz.y);
-      }
-      // intersect_rays (kernels.py:1242-1263) for this slot
+      // intersect_rays (kernels.py:1242-1263) for this ray
+      const float4 a = q_load(X.a + p);
+      const float2 dyz = h_load(X.d + p);
       float t = 0.0f;
       int32_t ref = 0;
-      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, o, d, kTMin, kTMax, st, t, ref);
+      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, pt_v3f(a.x, a.y, a.z), pt_v3f(a.w, dyz.x, dyz.y), kTMin,
+                                                       kTMax, st, t, ref);
       ++n_seg;
       if (!hit) ref = 0;
-      h_store(wb.hit + i, make_float2(t, __int_as_float(ref)));
+      h_store(X.hit + p, make_float2(t, __int_as_float(ref)));
       const int32_t list = hit ? leaf_class(ref) : kListEnded;
-      const uint32_t before = n_ended;
       if (list == kListEnded) {
-        end_unscattered(sc, fr, wb, i, w, ref);
+        end_unscattered(sc, fr, wb, X, p, s_load(X.item + p), ref);
         ++n_ended;
-      } else if (list == kListMedium || list == kListNoise) {
-        n_med += list == kListMedium ? 1u : 0u;
-        medium_entry<STACK, TRAV>(sc, fr, wb, st, i, list == kListNoise, n_ended, ends);
-      } else {
-        shade_entry(sc, fr, wb, list, i, n_ended, ends);
+        break;
       }
-      // the path ended (its slot now waits for work), or continues from its
-      // stored ray (the item word holds the item without kFresh)
-      w = n_ended != before ? kPending : (w & ~kFresh);
+      Cont cn;
+      cn.go = false;
+      if (list == kListMedium || list == kListNoise) {
+        n_med += list == kListMedium ? 1u : 0u;
+        medium_entry<STACK, TRAV>(sc, fr, wb, st, X, p, list == kListNoise, n_ended, ends, cn);
+      } else {
+        shade_entry(sc, fr, wb, X, list, p, n_ended, ends, cn);
+      }
+      if (!cn.go) break;  // the path ended (its colour is staged)
+      store_ray(X, p, cn);
     }
   }
   if (counters) {
@@ -895,17 +979,17 @@ __global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, W
 
 namespace {
 // Library-owned state of one device, created on first use: the streams and
-// fork/join events of pipes 1.., the live-count readback events and their
-// host-pinned slots [2][kPipes]. `mu` serialises ptmi_wf_render calls on the
-// device (each call drives all pipes and reads their counts back), so two
-// host threads rendering on one device never share readback slots; calls on
-// different devices run concurrently.
+// fork/join events of pipes 1.., the status readback events and their
+// host-pinned slots [2][kPipes][2]. `mu` serialises ptmi_wf_render calls on
+// the device (each call drives all pipes and reads their status back), so
+// two host threads rendering on one device never share readback slots; calls
+// on different devices run concurrently.
 struct PipeStreams {
   std::mutex mu;
   hipStream_t s[kPipes] = {};
   hipEvent_t fork = nullptr, join[kPipes] = {};
-  hipEvent_t rb[2][kPipes] = {};  // live-count readbacks of two consecutive chunks
-  int32_t* pinned_live = nullptr;
+  hipEvent_t rb[2][kPipes] = {};  // status readbacks of two consecutive chunks
+  int32_t* pinned = nullptr;      // [2][kPipes][2]: rays traced by the chunk's last wf_intersect, pool empty
   bool ok = false;
 };
 constexpr int kMaxDevices = 64;
@@ -915,7 +999,7 @@ PipeStreams g_pipes[kMaxDevices];
 hipError_t pipe_streams_init(PipeStreams* ps) {
   if (ps->ok) return hipSuccess;
   hipError_t e = hipSuccess;
-  if (!ps->pinned_live) e = hipHostMalloc((void**)&ps->pinned_live, 2 * kPipes * sizeof(int32_t), hipHostMallocDefault);
+  if (!ps->pinned) e = hipHostMalloc((void**)&ps->pinned, 2 * kPipes * 2 * sizeof(int32_t), hipHostMallocDefault);
   if (e == hipSuccess && !ps->fork) e = hipEventCreateWithFlags(&ps->fork, hipEventDisableTiming);
   for (int p = 1; p < kPipes && e == hipSuccess; ++p) {
     if (!ps->s[p]) e = hipStreamCreateWithFlags(&ps->s[p], hipStreamNonBlocking);
@@ -931,24 +1015,26 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
 #define PTMI_WF_RB_CHUNK 4  // A/B r04j: 4 +1.7 % C3, +1 % mesh fog over 8
 #endif
 #ifndef PTMI_WF_DRAIN_AT
-// A pipe whose read-back live count falls below capacity / drain_at finishes
-// its paths in one wf_drain launch (0 = never: one intersect and one scatter
-// launch per wave until the pipe is empty). The default; ptmi_wf_set_drain_at
-// changes it at run time (tests drive the tail with 1: drain as soon as the
-// pool is dry, while most groups still hold fetched items).
+// A pipe that traced fewer than capacity / drain_at rays after the pool ran
+// dry finishes its paths in one wf_drain launch (0 = never: one intersect
+// and one scatter launch per wave until the pipe is empty). The default;
+// ptmi_wf_set_drain_at changes it at run time (tests drive the tail with 1:
+// drain as soon as the pool is dry).
 #define PTMI_WF_DRAIN_AT 16
 #endif
 #ifndef PTMI_WF_CAPACITY_LOG2
-#define PTMI_WF_CAPACITY_LOG2 21  // queue slots (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
+#define PTMI_WF_CAPACITY_LOG2 21  // rays per iteration (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
 #endif
 constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
 std::atomic<int32_t> g_drain_at{PTMI_WF_DRAIN_AT};
 constexpr int32_t kSlotQuantum = kShards * kWfBlock;
 
-constexpr size_t kQueueBytesPerSlot = 48;
+// per ray position and parity: a 16, c 16, d 8, hit 8, item 4, ctr 4 bytes
+constexpr size_t kPosBytes = 56;
 struct Layout {
-  int32_t capacity, medseg;
-  size_t q, hit, lists, grp, staging, spill, ctl, total;
+  int32_t capacity, cp, seg_cap, npos, medseg;
+  size_t rb, lists, staging, spill, ctl, total;
+  size_t rb_pipe, lists_pipe;
 };
 constexpr size_t kSpillPipeBytes = (size_t)kSpillSlots * (PTMI_WF_MAX_BLOCKS / kPipes) * kWfBlock * 8;
 
@@ -958,14 +1044,21 @@ Layout layout(int32_t npix, int32_t batch) {
   int64_t cap = npix > kMaxCapacity ? npix : kMaxCapacity;
   if (items < cap) cap = items;
   cap = (cap + kPipes * kSlotQuantum - 1) / (kPipes * kSlotQuantum) * (kPipes * kSlotQuantum);
-  L.capacity = (int32_t)cap;  // all pipes; each pipe has capacity / kPipes slots
-  L.medseg = (int32_t)(cap / kPipes / kShards);
-  size_t c = (size_t)cap;
-  L.q = 0;  // queue streams: A (16 B), D (8 B), C (16 B), item (4 B), ctr (4 B) per slot
-  L.hit = L.q + kQueueBytesPerSlot * c;
-  L.lists = L.hit + sizeof(float2) * c;
-  L.grp = (L.lists + 4 * sizeof(int32_t) * c + 15) & ~(size_t)15;
-  L.staging = (L.grp + sizeof(int2) * (c / 64) + 15) & ~(size_t)15;
+  L.capacity = (int32_t)cap;  // all pipes
+  L.cp = (int32_t)(cap / kPipes);
+  int64_t sc = ((int64_t)L.cp / PTMI_WF_SEG_DIV + 63) / 64 * 64;
+  L.seg_cap = (int32_t)(sc < 64 ? 64 : sc);
+  L.npos = kSegs * L.seg_cap + 2 * L.cp;
+  // a shard's blocks take every kShards-th 128-entry chunk of wf_intersect's
+  // work (<= cp + the bins' and the overflow's padding): a list segment holds them all
+  const int64_t work = (int64_t)L.cp + 64ll * (kBins + 1);
+  const int64_t chunks = (work + kWfBlock - 1) / kWfBlock;
+  L.medseg = (int32_t)((chunks + kShards - 1) / kShards * kWfBlock);
+  L.rb_pipe = 2 * kPosBytes * (size_t)L.npos;
+  L.lists_pipe = 4 * kShards * sizeof(int32_t) * (size_t)L.medseg;
+  L.rb = 0;
+  L.lists = L.rb + kPipes * L.rb_pipe;
+  L.staging = (L.lists + kPipes * L.lists_pipe + 255) & ~(size_t)255;
   L.spill = (L.staging + 3 * sizeof(float) * (size_t)items + 255) & ~(size_t)255;
   L.ctl = L.spill + kPipes * kSpillPipeBytes;
   L.total = L.ctl + kCtlWords * sizeof(int32_t);
@@ -976,20 +1069,21 @@ Layout layout(int32_t npix, int32_t batch) {
 static_assert((PTMI_WF_MAX_BLOCKS / kPipes) % kShards == 0, "a pipe's grid must be a multiple of the shard count");
 
 // One batch: generate on the caller's stream, fork the pipes, run each pipe's
-// intersect -> scatter loop on its own stream until its slots have all
-// retired, join, resolve.
+// intersect -> scatter loop on its own stream until its rays have all ended
+// and the pool is empty, join, resolve.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
 static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs* wbs, float* accum, int32_t batch,
                            unsigned long long* counters, hipStream_t stream, const PipeStreams& ps) {
-  // a pipe's grid = multiple of kShards and of the slot quantum, so its slot i
-  // always maps to block (i / kWfBlock) % grid with shard (i / kWfBlock) % kShards
+  // a pipe's grid = a multiple of kShards, so block b's shard is b % kShards
   int64_t blocks = wbs[0].capacity / kWfBlock;
   if (blocks > PTMI_WF_MAX_BLOCKS / kPipes) blocks = PTMI_WF_MAX_BLOCKS / kPipes;
   const unsigned g = (unsigned)blocks;
+  // the tail launch: one lane per continuing ray (<= capacity + the bins' padding)
+  const unsigned gd = (unsigned)((wbs[0].capacity + 64 * (kBins + 1) + kWfBlock - 1) / kWfBlock);
   (void)hipMemsetAsync(wbs[0].next, 0, kCtlWords * sizeof(int32_t), stream);
-  for (int p = 0; p < kPipes; ++p) {
+  {
     const int pslot = prof_begin(kProfWfGenerate, stream);
-    hipLaunchKernelGGL(wf_generate, dim3(g), dim3(kWfBlock), 0, stream, fr, wbs[p], (int32_t)(p == 0));
+    hipLaunchKernelGGL(wf_generate, dim3(1), dim3(64), 0, stream, wbs[0]);
     prof_end(pslot, stream);
   }
   hipStream_t st[kPipes];
@@ -1001,19 +1095,19 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     if (e != hipSuccess) return e;
   }
   // Each item needs at most max_depth waves and every iteration advances every
-  // live ray by one wave (or hands a waiting slot an item), so this many
-  // iterations always drain a pipe.
-  const int64_t max_iters = (int64_t)wbs[0].nunits * 64 * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 2;
+  // live ray by one wave (or starts a new item), so this many iterations
+  // always drain a pipe.
+  const int64_t max_iters = (int64_t)wbs[0].nitems * (int64_t)(fr.max_depth > 0 ? fr.max_depth : 1) + 2;
   bool live[kPipes];
   for (int p = 0; p < kPipes; ++p) live[p] = true;
   int64_t it = 0;
-  const int32_t chunk = PTMI_WF_RB_CHUNK;  // iterations between live-count readbacks
+  const int32_t chunk = PTMI_WF_RB_CHUNK;  // iterations between status readbacks
   const int64_t drain_at = g_drain_at.load(std::memory_order_relaxed);
   hipError_t err = hipSuccess;
-  // The host reads chunk k's live counts only after chunk k + 1 is queued, so
-  // the pipes never idle through the readback's host round trip. Iterations
-  // on a drained pipe are no-ops (no slot holds or receives work), so the one
-  // extra chunk a pipe may run after draining changes nothing.
+  // The host reads chunk k's status only after chunk k + 1 is queued, so the
+  // pipes never idle through the readback's host round trip. Iterations on a
+  // drained pipe are no-ops (no ray left, no item to claim), so the one extra
+  // chunk a pipe may run after draining changes nothing.
   bool inflight[2][kPipes] = {};
   int cur = 0;
   while (it < max_iters) {
@@ -1022,7 +1116,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
       for (int p = 0; p < kPipes; ++p) {
         if (!live[p]) continue;
         const WfBufs& wb = wbs[p];
-        const int32_t par = (int32_t)((it + j) & 1);  // which list counters this iteration uses
+        const int32_t par = (int32_t)((it + j) & 1);  // which ray buffer and list counters this iteration uses
         const int ps_i = prof_begin(kProfWfIntersect, st[p]);
         hipLaunchKernelGGL((wf_intersect<STACK, TRAV>), dim3(g), dim3(kWfBlock), 0, st[p], sc, fr, wb, par, counters);
         prof_end(ps_i, st[p]);
@@ -1036,7 +1130,7 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
       inflight[cur][p] = live[p];
       if (!live[p]) continue;
-      err = hipMemcpyAsync(ps.pinned_live + cur * kPipes + p, ctl_live(wbs[p]), sizeof(int32_t),
+      err = hipMemcpyAsync(ps.pinned + (cur * kPipes + p) * 2, ctl_status(wbs[p]), 2 * sizeof(int32_t),
                            hipMemcpyDeviceToHost, st[p]);
       if (err == hipSuccess) err = hipEventRecord(ps.rb[cur][p], st[p]);
     }
@@ -1053,15 +1147,17 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
     bool any = false;
     for (int p = 0; p < kPipes && err == hipSuccess; ++p) {
       if (inflight[prev][p]) {
-        const int32_t n_live = ps.pinned_live[prev * kPipes + p];
-        live[p] = live[p] && n_live != 0;
-        if (live[p] && drain_at > 0 && (int64_t)n_live * drain_at < (int64_t)wbs[p].capacity) {
-          // the pool is empty (some slot found no work) and few paths are left:
-          // finish them, and the items groups still hold, in one launch,
-          // queued behind the iterations in flight
+        const int32_t traced = ps.pinned[(prev * kPipes + p) * 2], dry = ps.pinned[(prev * kPipes + p) * 2 + 1];
+        // the pool was empty before that iteration began, so it claimed no
+        // item and traced only its continuing rays: none means the pipe is done
+        if (dry && traced == 0) live[p] = false;
+        if (live[p] && dry && drain_at > 0 && (int64_t)traced * drain_at < (int64_t)wbs[p].capacity) {
+          // few paths left and no work to add: finish them in one launch,
+          // queued behind the iterations in flight, on the rays the next
+          // iteration would trace
           const int pd = prof_begin(kProfWfDrain, st[p]);
-          hipLaunchKernelGGL((wf_drain<STACK, TRAV>), dim3((unsigned)(wbs[p].capacity / kWfBlock)), dim3(kWfBlock), 0,
-                             st[p], sc, fr, wbs[p], counters);
+          hipLaunchKernelGGL((wf_drain<STACK, TRAV>), dim3(gd), dim3(kWfBlock), 0, st[p], sc, fr, wbs[p],
+                             (int32_t)(it & 1), counters);
           prof_end(pd, st[p]);
           err = hipGetLastError();
           live[p] = false;
@@ -1102,11 +1198,13 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
                      hipStream_t stream) {
   const int32_t npix = fr.w * fr.n_rows;
   // work items (sample, pixel) of a batch are ids below 2^31 (FastDiv's
-  // range), padded ids included: 64 per 8x8 pixel square, and the batch's
-  // samples rounded up to whole chunks (wb.nunits below)
+  // range, and the kFresh bit), padded ids included: 64 per 8x8 pixel square,
+  // and the batch's samples rounded up to whole chunks (wb.nitems below); the
+  // pool counters may run past their shard's end by the lanes asking at once
+  // (< 2^24 in all)
   const int64_t sq_items = 64ll * ((fr.w + 7) / 8) * ((fr.n_rows + 7) / 8);
   int32_t batch = s_count;
-  const int64_t max_batch = sq_items > 0 ? 0x7fffffffll / sq_items - (PTMI_WF_CHUNK_SAMPLES - 1) : 0;
+  const int64_t max_batch = sq_items > 0 ? (0x7fffffffll - (1ll << 24)) / sq_items - (PTMI_WF_CHUNK_SAMPLES - 1) : 0;
   if (batch > max_batch) batch = (int32_t)max_batch;
   if (batch < 1) return hipErrorInvalidValue;
   while (batch > 1 && layout(npix, batch).total > ws_bytes) batch = (batch + 1) / 2;
@@ -1127,32 +1225,36 @@ hipError_t wf_render(const DevScene& sc, const DevFrame& fr, int32_t stack_neede
     const int32_t nb = s_count - b0 < batch ? s_count - b0 : batch;
     const Layout L = layout(npix, nb);
     char* base = (char*)ws;
-    const size_t c = (size_t)L.capacity, cp = c / kPipes;
+    const size_t np = (size_t)L.npos;
     WfBufs wbs[kPipes];
     for (int p = 0; p < kPipes; ++p) {
       WfBufs& wb = wbs[p];
-      wb.q.a = (float4*)(base + L.q) + p * cp;
-      wb.q.d = (float2*)(base + L.q + 16 * c) + p * cp;
-      wb.q.c = (float4*)(base + L.q + 24 * c) + p * cp;
-      wb.q.item = (uint32_t*)(base + L.q + 40 * c) + p * cp;
-      wb.q.ctr = (uint32_t*)(base + L.q + 44 * c) + p * cp;
-      wb.hit = (float2*)(base + L.hit) + p * cp;
-      wb.lists = (int32_t*)(base + L.lists) + p * 4 * cp;
-      wb.grp = (int2*)(base + L.grp) + p * (cp / 64);
+      char* rbp = base + L.rb + p * L.rb_pipe;
+      for (int q = 0; q < 2; ++q) {
+        char* r = rbp + q * kPosBytes * np;
+        wb.rb[q].a = (float4*)r;
+        wb.rb[q].c = (float4*)(r + 16 * np);
+        wb.rb[q].d = (float2*)(r + 32 * np);
+        wb.rb[q].hit = (float2*)(r + 40 * np);
+        wb.rb[q].item = (uint32_t*)(r + 48 * np);
+        wb.rb[q].ctr = (uint32_t*)(r + 52 * np);
+      }
+      wb.lists = (int32_t*)(base + L.lists + p * L.lists_pipe);
       wb.staging = (float*)(base + L.staging);
       wb.next = (int32_t*)(base + L.ctl);
       wb.ctl = wb.next + (8 + p * kPipeLines) * kLine;
       wb.spill = base + L.spill + p * kSpillPipeBytes;
-      wb.capacity = (int32_t)cp;
+      wb.capacity = L.cp;
+      wb.seg_cap = L.seg_cap;
       wb.medseg = L.medseg;
       wb.npix = npix;
       wb.sq_x = (fr.w + 7) / 8;
       wb.nsq = wb.sq_x * ((fr.n_rows + 7) / 8);
       wb.batch = nb;
       wb.csamp = nb < PTMI_WF_CHUNK_SAMPLES ? nb : PTMI_WF_CHUNK_SAMPLES;
-      wb.nunits = wb.nsq * ((nb + wb.csamp - 1) / wb.csamp) * wb.csamp;
-      wb.shard_len = (wb.nunits / wb.csamp + kShards - 1) / kShards * wb.csamp;
-      wb.shard_groups = L.capacity / 64 / kShards;  // all pipes draw on every shard
+      const int32_t nchunks = wb.nsq * ((nb + wb.csamp - 1) / wb.csamp);
+      wb.nitems = nchunks * 64 * wb.csamp;
+      wb.shard_len = (nchunks + kShards - 1) / kShards * 64 * wb.csamp;
       wb.s_begin = s_begin + b0;
       wb.by_per = fast_div(64u * (uint32_t)wb.csamp);
       wb.by_nsq = fast_div((uint32_t)wb.nsq);

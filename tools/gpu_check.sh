@@ -19,6 +19,7 @@
 #   abtrace_<lib>_<mk|wf> rocprofv3 kernel trace + stats of tools/ab.py (64 spp x 2) with variants/libptmi_<lib>.so
 #                         (<lib> = default: the default build)
 #   abpmc_<lib>_<mk|wf>   FETCH_SIZE, WRITE_SIZE and cache-hit PMC passes of tools/ab.py (32 spp x 1), same libs
+#   ablat_<lib>_<mk|wf>   the VALU / wait PMC passes (tools/gpu_pmc_latency.sh) with variants/libptmi_<lib>.so
 #   probe                 the diagnostic probe builds (tools/gpu_probe.sh; variants libptmi_probe{1,2}.so)
 # Every step has its own time limit; the script stops at the first failure.
 set -u
@@ -63,6 +64,9 @@ for s in $STEPS; do
       PTMI_LIB=$PWD/$lib step ${s}_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/abpmc" -o ${name}_${mode}_fetch -- python tools/ab.py $mode 32 1 &&
       PTMI_LIB=$PWD/$lib step ${s}_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/abpmc" -o ${name}_${mode}_write -- python tools/ab.py $mode 32 1 &&
       PTMI_LIB=$PWD/$lib step ${s}_cache 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/abpmc" -o ${name}_${mode}_cache -- python tools/ab.py $mode 32 1 ;;
+    ablat_*) r=${s#ablat_}; name=${r%_*}; mode=${r##*_}
+      lib=path-tracer-python_amd/ptmi/_lib/libptmi.so; [ "$name" = default ] || lib=path-tracer-python_amd/ptmi/_lib/variants/libptmi_$name.so
+      PTMI_LIB=$PWD/$lib step $s 600 env PMC_VARIANT=$mode PMC_DIR=$OUT/ablat_$name bash tools/gpu_pmc_latency.sh ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
