@@ -328,13 +328,25 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
   return false;
 }
 
+#ifndef PTMI_TRI_E2Z_DWORD
+#define PTMI_TRI_E2Z_DWORD 0
+#endif
 __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
                                           float tmax, float& t) {
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
-  pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1], C = ((const pt_f4*)tr)[2];
+  pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1];
+#if PTMI_TRI_E2Z_DWORD
+  // the test reads e2.z of the third 16 B only (the normal is read at shading)
+  float cx = ((const float*)tr)[8];
+  asm volatile("" : "+v"(A), "+v"(B), "+v"(cx));
+  return hit_tri_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w), make_float4(cx, 0.0f, 0.0f, 0.0f),
+                   o, d, tmin, tmax, t);
+#else
+  pt_f4 C = ((const pt_f4*)tr)[2];
   asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
   return hit_tri_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
                    make_float4(C.x, C.y, C.z, C.w), o, d, tmin, tmax, t);
+#endif
 }
 
 __device__ __forceinline__ bool hit_leaf(const DevScene& sc, int32_t ref, pt_v3 o, pt_v3 d, float tmin,
@@ -486,7 +498,11 @@ __device__ unsigned long long g_probe[16];
 // last 16 B hold them precomputed and are not read. A/B on MI355X (round 4,
 // parity-identical): a 64-B stride without them, C2 -1.2 %, C4 -1.1 %, C5
 // -0.7 %, C3 +-0 (profiles/r04/ab/ab_r04z_node64.log), so the stride stays 80.
-constexpr uint32_t kNodeBytes = 80;
+#ifndef PTMI_NODE_BYTES
+#define PTMI_NODE_BYTES 80
+#endif
+static_assert(PTMI_NODE_BYTES == 80 || PTMI_NODE_BYTES == 64, "node stride: 80 or 64 B");
+constexpr uint32_t kNodeBytes = PTMI_NODE_BYTES;
 
 // In-flight traversal of one ray: begin (root test, push root) and one pop
 // of the loop per step, so a kernel can interleave steps of different rays'

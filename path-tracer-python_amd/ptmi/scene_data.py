@@ -12,6 +12,7 @@ texels) documented in include/ptmi.h.
 """
 from __future__ import annotations
 
+import collections
 import json
 import os
 from dataclasses import dataclass, field
@@ -182,6 +183,16 @@ CLASS_LAMBERTIAN, CLASS_GLOSSY, CLASS_DIELECTRIC, CLASS_MEDIUM, CLASS_NOISE, CLA
 
 NODE_FLOATS = 20  # 80-B internal node (include/ptmi.h)
 NODE_BYTES = 4 * NODE_FLOATS  # an internal child ref is the child's byte offset in the node array
+# Node strides a library build may use (ptmi_node_bytes()): 80 (both
+# children's x / y centres stored in the last 16 B, not read) or 64 (without
+# them: the kernels compute them from the boxes either way).
+NODE_STRIDES = (64, 80)
+# Placement of the internal nodes in the node array (refs are byte offsets,
+# so any placement walks the same tree in the same order): the reference's
+# preorder; breadth first (a node's two internal children adjacent); or
+# "pairs", depth first over sibling pairs (children adjacent, each subtree
+# contiguous). With 64-B nodes the pairs start on 128-B lines.
+NODE_ORDERS = ('preorder', 'bfs', 'pairs')
 
 
 def leaf_code(prim_type, prim_idx, mat_class=0):
@@ -237,9 +248,12 @@ class DeviceLayout:
     def num_bvh_nodes(self):
         return 0 if self.ref_nodes is None else int(self.ref_nodes.shape[0])
 
+    # internal nodes (the node array may hold unused padding rows besides)
+    n_internal: int = None
+
     @property
     def n_inner(self):
-        return int(self.nodes.shape[0])
+        return int(self.nodes.shape[0]) if self.n_internal is None else int(self.n_internal)
 
     def nbytes(self):
         return sum(int(a.nbytes) for a in (self.nodes, self.spheres, self.quads, self.tris, self.mats,
@@ -341,7 +355,39 @@ def ref_layout_nodes(bvh, codes):
     return out
 
 
-def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True) -> DeviceLayout:
+def node_slots(left, right, is_leaf, order='preorder', align_pairs=False):
+    """Slot (row of the node array) of every internal node, by reference node
+    index (-1 for leaves), and the number of rows (NODE_ORDERS). align_pairs:
+    two internal siblings start on an even row (a 128-B line of 64-B nodes);
+    a skipped row is padding no ref points to."""
+    n = left.shape[0]
+    internal = ~is_leaf
+    slot = np.full(n, -1, np.int64)
+    if order not in NODE_ORDERS:
+        raise ValueError(f'unknown node order {order!r} (one of {NODE_ORDERS})')
+    if order == 'preorder' or n == 0 or not internal[0]:
+        idx = np.nonzero(internal)[0]
+        slot[idx] = np.arange(idx.shape[0])
+        return slot, int(idx.shape[0])
+
+    def kids(i):
+        return [int(c) for c in (left[i], right[i]) if c >= 0 and internal[c]]
+    slot[0], k = 0, 1
+    todo = collections.deque([0])
+    while todo:
+        i = todo.popleft() if order == 'bfs' else todo.pop()
+        ch = kids(i)
+        if align_pairs and len(ch) == 2 and k % 2:
+            k += 1
+        for c in ch:
+            slot[c] = k
+            k += 1
+        todo.extend(ch if order == 'bfs' else reversed(ch))  # pairs: the left subtree first
+    return slot, k
+
+
+def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True,
+                node_order: str = 'preorder') -> DeviceLayout:
     """Reference-layout arrays -> include/ptmi.h device layout. ``node_bytes``
     is the library's node stride (ptmi_node_bytes(): 80, one child record
     per internal node). Each leaf code carries its primitive's material
@@ -387,25 +433,28 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
         cls = np.where(is_leaf, material_class(mats[rows, 19].view(np.uint32)) if len(mats) else 0, 0)
     codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | (cls << LEAF_INDEX_BITS) | new_idx)
              - (1 << 32)).astype(np.int32)
-    if node_bytes != NODE_BYTES:
+    if node_bytes not in NODE_STRIDES:
         raise ValueError(f'unsupported node stride {node_bytes}')
-    if internal.shape[0] * node_bytes > 0x7fffffff:
-        raise ValueError(f'{internal.shape[0]} internal BVH nodes: byte offsets exceed int32')
+    cidx, nrows = node_slots(left, right, is_leaf, node_order, align_pairs=node_bytes == 64)
+    if nrows * node_bytes > 0x7fffffff:
+        raise ValueError(f'{nrows} BVH node rows: byte offsets exceed int32')
     refs = np.where(is_leaf, codes, (cidx * node_bytes).astype(np.int32)).astype(np.int32)
-    nodes = np.zeros((internal.shape[0], NODE_FLOATS), np.float32)
+    nodes = np.zeros((nrows, node_bytes // 4), np.float32)
     if internal.size:  # children interleaved per component (include/ptmi.h)
         l, r = left[internal], right[internal]
-        nodes[:, 0:12:2] = np.concatenate([bmin[l], bmax[l]], axis=1)
-        nodes[:, 1:12:2] = np.concatenate([bmin[r], bmax[r]], axis=1)
-        nodes[:, 12] = refs[l].view(np.float32)
-        nodes[:, 13] = refs[r].view(np.float32)
+        rows = cidx[internal]
+        nodes[rows, 0:12:2] = np.concatenate([bmin[l], bmax[l]], axis=1)
+        nodes[rows, 1:12:2] = np.concatenate([bmin[r], bmax[r]], axis=1)
+        nodes[rows, 12] = refs[l].view(np.float32)
+        nodes[rows, 13] = refs[r].view(np.float32)
         # box centres (min + max) * 0.5 in f32 — the same rounding as the
         # kernels' (kernels.py:707-710), so precomputing them changes nothing
         cl = (bmin[l] + bmax[l]) * np.float32(0.5)
         cr = (bmin[r] + bmax[r]) * np.float32(0.5)
-        nodes[:, 14], nodes[:, 15] = cl[:, 2], cr[:, 2]
-        nodes[:, 16], nodes[:, 17] = cl[:, 0], cr[:, 0]
-        nodes[:, 18], nodes[:, 19] = cl[:, 1], cr[:, 1]
+        nodes[rows, 14], nodes[rows, 15] = cl[:, 2], cr[:, 2]
+        if node_bytes == 80:
+            nodes[rows, 16], nodes[rows, 17] = cl[:, 0], cr[:, 0]
+            nodes[rows, 18], nodes[rows, 19] = cl[:, 1], cr[:, 1]
     ref_nodes = ref_layout_nodes(b, np.where(is_leaf, codes, 0).astype(np.int32))
     if n:
         root_ref = int(refs[0])
@@ -449,7 +498,7 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
     if pperm.min() < 0 or pperm.max() > 255:
         raise ValueError('Perlin permutation out of range')
     return DeviceLayout(nodes, root_ref, root_min, root_max, max_leaf_depth, spheres, quads, tris, mats,
-                        texels, offs, ws, hs, pv, pperm, ns, nq, nt, perm, ref_nodes)
+                        texels, offs, ws, hs, pv, pperm, ns, nq, nt, perm, ref_nodes, int(internal.shape[0]))
 
 
 def compile_world(world, perlin_tables=None):
