@@ -577,6 +577,149 @@ __device__ __forceinline__ void append_list(const WfBufs& wb, int32_t par, int32
   if (list >= 0 && k < wb.medseg) s_store(list_slot(wb, list, shard, k), p);  // always < medseg: it bounds a shard's rays
 }
 
+#ifndef PTMI_WF_REFILL
+// 1: each wf_intersect wave works through a chunk of one section of the
+// work (a direction bin, the overflow region or the fresh rays) and refills
+// the lanes whose traversal has ended with the chunk's next rays, retiring
+// finished lanes (classification, list append) once at most
+// PTMI_WF_REFILL_AT lanes are still traversing — the megakernel's decoupled
+// step loop, on rays that are neighbours in their sorted segment. 0: one ray
+// per lane per 64-entry slice of the work.
+#define PTMI_WF_REFILL 0
+#endif
+#ifndef PTMI_WF_REFILL_AT
+#define PTMI_WF_REFILL_AT 16
+#endif
+#if PTMI_WF_REFILL
+// A lane's ray: continuing (position p of a segment or of the overflow
+// region) or fresh (item claimed, camera ray generated).
+template <int STACK, int TRAV, int LDS>
+__device__ __forceinline__ void wf_intersect_refill(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
+                                                    int32_t par, int32_t shard, const SegTable& T, int32_t nfresh,
+                                                    Stack st, uint32_t& n_live, uint32_t& n_ended) {
+  const RayBuf& X = wb.rb[par];
+  const int lane = lane_id();
+  // chunks: each bin's entries, the overflow entries and the fresh rays cut
+  // into pieces of ch entries (one piece per wave of the grid, about)
+  const int32_t waves = (int32_t)(gridDim.x * (kWfBlock / 64));
+  const int32_t total = T.live + nfresh;
+  const int32_t ch = max(64, ((total + waves - 1) / waves + 63) & ~63);
+  // lane b < kBins: chunks of bin b; then the overflow's and the fresh rays'
+  const int32_t nb = lane < kBins ? (T.btot + ch - 1) / ch : 0;
+  const int32_t nb_incl = wave_incl_scan(nb);
+  const int32_t bin_chunks = __shfl(nb_incl, 63);
+  const int32_t ovf_chunks = (T.ovf_n + ch - 1) / ch, fresh_chunks = (nfresh + ch - 1) / ch;
+  const int32_t nchunks = bin_chunks + ovf_chunks + fresh_chunks;
+  typename TravOf<TRAV>::T tr;
+  tr.init(st);
+  for (int32_t q = (int32_t)(blockIdx.x * (kWfBlock / 64) + (threadIdx.x >> 6)); q < nchunks; q += waves) {
+    // the chunk's section (wave-uniform): bin b, the overflow (-1) or the fresh rays (-2), and its entry range
+    int32_t b = -2, lo = 0, hi = 0;
+    if (q < bin_chunks) {
+      const unsigned long long m = pt_ballot(lane < kBins && nb_incl > q);
+      b = __ffsll((long long)m) - 1;
+      const int32_t first = __builtin_amdgcn_readlane(nb_incl, b) - __builtin_amdgcn_readlane(nb, b);
+      lo = (q - first) * ch;
+      hi = min(lo + ch, __builtin_amdgcn_readlane(T.btot, b));
+    } else if (q < bin_chunks + ovf_chunks) {
+      b = -1;
+      lo = (q - bin_chunks) * ch;
+      hi = min(lo + ch, T.ovf_n);
+    } else {
+      lo = (q - bin_chunks - ovf_chunks) * ch;
+      hi = min(lo + ch, nfresh);
+    }
+    int32_t cursor = lo;  // wave-uniform: the chunk's next entry
+    bool act = false;     // the lane holds a ray (traversing, or traced and not yet retired)
+    int32_t p = -1;
+    uint32_t item = 0u;
+    pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
+    for (;;) {
+      // refill the lanes without a ray from the chunk
+      const unsigned long long need = pt_ballot(!act);
+      if (need != 0ull && cursor < hi) {
+        const int32_t rank = (int32_t)lane_rank(need), n = (int32_t)__popcll(need);
+        const int32_t j = cursor + rank;
+        const bool take = !act && j < hi;
+        cursor = min(cursor + n, hi);
+        int32_t np = -1;
+        if (b >= 0 || b == -1) {
+          if (take) {
+            if (b == -1) {
+              np = ovf_base(wb) + j;
+            } else {
+              int32_t s = 0, off = j;
+#pragma unroll
+              for (int k = 1; k < kShards; ++k) {
+                const int32_t pk = __builtin_amdgcn_readlane(T.pre, b * kShards + k);
+                if (j >= pk) {
+                  s = k;
+                  off = j - pk;
+                }
+              }
+              np = (b * kShards + s) * wb.seg_cap + off;
+            }
+            item = s_load(X.item + np);
+            const float4 a = q_load(X.a + np);
+            const float2 dyz = h_load(X.d + np);
+            o = pt_v3f(a.x, a.y, a.z);
+            d = pt_v3f(a.w, dyz.x, dyz.y);
+          }
+        } else {  // generate_camera_rays (kernels.py:1219-1239) for the next work items
+          const int32_t k = claim_items(wb, shard, take);
+          if (k >= 0) {
+            const Item it = decode_item(fr, wb, (uint32_t)k);
+            if (it.valid) {
+              Rng rng{path_key(fr, wb, it), 0u};
+              get_ray(fr, it.px, it.py, rng, o, d);  // direction left unnormalized (Q1)
+              np = fresh_base(wb) + j;
+              item = (uint32_t)k | kFresh;
+              s_store(X.item + np, item);
+            }
+          }
+        }
+        if (np >= 0) {
+          p = np;
+          act = true;
+          ++n_live;
+          trav_begin<STACK, kWfBlock>(sc, tr, st, d, o, kTMin, kTMax);
+        }
+      }
+      if (pt_ballot(act) == 0ull) {
+        if (cursor >= hi) break;
+        continue;
+      }
+      // traversal steps until few lanes are still traversing
+      for (;;) {
+        const unsigned long long mbusy = pt_ballot(tr.busy());
+        const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
+        if (nbusy == 0) break;
+        if (nbusy <= (uint32_t)PTMI_WF_REFILL_AT && pt_ballot(act && !tr.busy()) != 0ull) break;
+#pragma unroll
+        for (int u = 0; u < PTMI_TRAV_UNROLL; ++u)
+          if (tr.busy()) trav_step<STACK, kWfBlock, 0, LDS>(sc, sc.nodes, tr, st, o, d);
+      }
+      // retire the lanes whose traversal has ended: classify
+      const bool fin = act && !tr.busy();
+      int32_t list = -1;
+      if (fin) {
+        const int32_t ref = tr.any() ? tr.best : 0;  // 0: a miss
+        list = tr.any() ? leaf_class(ref) : kListEnded;
+        if (list == kListEnded) {
+          end_unscattered(sc, fr, wb, X, p, item, ref);
+          ++n_ended;
+          list = -1;
+        } else {
+          h_store(X.hit + p, make_float2(tr.closest, __int_as_float(ref)));
+        }
+        act = false;
+      }
+      append_list(wb, par, shard, list, p);
+    }
+  }
+}
+#endif
+
 // intersect_rays, kernels.py:1242-1263, plus the closest-hit classification:
 // a miss (shade_miss_rays, kernels.py:1266-1280) or an emissive hit
 // (kernels.py:1365-1375) ends its path here; every other traced ray is
@@ -608,6 +751,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
     ctl_status(wb)[1] = dry ? 1 : 0;
   }
   uint32_t n_live = 0, n_ended = 0;
+#if PTMI_WF_REFILL
+  (void)stride;
+  wf_intersect_refill<STACK, TRAV, LDS>(sc, fr, wb, par, shard, T, nfresh, st, n_live, n_ended);
+#else
   for (int32_t w0 = (int32_t)(blockIdx.x * kWfBlock) + (tid & ~63); w0 < nwork; w0 += stride) {
     int32_t p = -1;
     uint32_t item = 0u;
@@ -653,6 +800,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
     }
     append_list(wb, par, shard, list, p);
   }
+#endif
   if (counters) {
     block_flush<1>({n_live}, lds_stack, counters + 0);
     block_flush<1>({n_ended}, lds_stack, counters + 2);
