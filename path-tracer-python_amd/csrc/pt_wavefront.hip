@@ -109,9 +109,13 @@ constexpr int kWfBlock = PTMI_WF_BLOCK;
 #define PTMI_WF_SPILL_MAX_STACK 20  // kernels of 17 to this many stack slots spill; deeper ones keep them all in LDS
 #endif
 constexpr int kSpillSlots = PTMI_WF_SPILL_MAX_STACK > PTMI_WF_ISECT_LDS ? PTMI_WF_SPILL_MAX_STACK - PTMI_WF_ISECT_LDS : 0;
+#ifndef PTMI_WF_SPILL_MIN_STACK
+#define PTMI_WF_SPILL_MIN_STACK 17  // kernels of this many stack slots up to PTMI_WF_SPILL_MAX_STACK spill
+#endif
 template <int STACK, int TRAV>
 constexpr int isect_lds() {
-  return (TRAV == PTMI_TRAV_STACK && STACK > 16 && STACK <= PTMI_WF_SPILL_MAX_STACK && PTMI_WF_ISECT_LDS < STACK)
+  return (TRAV == PTMI_TRAV_STACK && STACK >= PTMI_WF_SPILL_MIN_STACK && STACK <= PTMI_WF_SPILL_MAX_STACK &&
+          PTMI_WF_ISECT_LDS < STACK)
              ? PTMI_WF_ISECT_LDS
              : STACK;
 }

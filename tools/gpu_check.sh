@@ -15,6 +15,7 @@
 #   parity_variants  the GPU parity tests against each variants/*.so
 #   cache_mk / cache_wf   L1/L2 hit-rate PMC pass of one 32-spp call (tools/pmc_cache_summary.py reads it)
 #   lat_mk / lat_wf       VALU / wait PMC passes (tools/gpu_pmc_latency.sh; tools/pmc_valu.py reads them)
+#   latc4_mk / latc4_wf / latc5_mk   the same on the C4 mesh-fog scene / the C5 4K scene
 #   ta_mk / ta_wf         texture-address (vector memory address) unit busy cycles of one 32-spp call
 #   abtrace_<lib>_<mk|wf> rocprofv3 kernel trace + stats of tools/ab.py (64 spp x 2) with variants/libptmi_<lib>.so
 #                         (<lib> = default: the default build)
@@ -55,6 +56,8 @@ for s in $STEPS; do
     cache_mk|cache_wf) v=${s#cache_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_cache" -o $v -- python tools/ab.py $v 32 1 ;;
     ta_mk|ta_wf) v=${s#ta_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_ta" -o $v -- python tools/ab.py $v 32 1 ;;
     lat_mk|lat_wf) v=${s#lat_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_$v bash tools/gpu_pmc_latency.sh ;;
+    latc4_mk|latc4_wf) v=${s#latc4_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_c4_$v PMC_SCENE_ARGS="cornell_mesh_fog 1024" bash tools/gpu_pmc_latency.sh ;;
+    latc5_mk) step $s 600 env PMC_VARIANT=mk PMC_DIR=$OUT/pmc_latency_c5_mk PMC_SCENE_ARGS="vol2_final_scene_comparison 3840" bash tools/gpu_pmc_latency.sh ;;
     probe) step probe 600 bash tools/gpu_probe.sh ;;
     abtrace_*) r=${s#abtrace_}; name=${r%_*}; mode=${r##*_}
       lib=path-tracer-python_amd/ptmi/_lib/libptmi.so; [ "$name" = default ] || lib=path-tracer-python_amd/ptmi/_lib/variants/libptmi_$name.so
