@@ -12,6 +12,8 @@
 #                the default build: wavefront on vol2 800x800 or the mesh-fog
 #                scene, megakernel on C2 / C4 / C5 shapes
 #                (WF_VARIANTS / MK_VARIANTS="a b": only variants/libptmi_{a,b}.so)
+#   ab_wf_both   wavefront A/B (three calls per lib and round) on C3 and on the mesh-fog scene
+#   wftests      the wavefront / parity / edge subset of the GPU suite (PTMI_LIB: another build)
 #   parity_variants  the GPU parity tests against each variants/*.so
 #   cache_mk / cache_wf   L1/L2 hit-rate PMC pass of one 32-spp call (tools/pmc_cache_summary.py reads it)
 #   lat_mk / lat_wf       VALU / wait PMC passes (tools/gpu_pmc_latency.sh; tools/pmc_valu.py reads them)
@@ -51,6 +53,9 @@ for s in $STEPS; do
     ab_mk_c2) step $s 900 env AB_MODES=mk AB_VARIANTS="${MK_VARIANTS:-}" bash tools/gpu_ab.sh ;;
     ab_mk_c4) step $s 900 env AB_MODES=mk AB_VARIANTS="${MK_VARIANTS:-}" AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh ;;
     ab_mk_c5) step $s 900 env AB_MODES=mk AB_VARIANTS="${MK_VARIANTS:-}" AB_SCENE=vol2_final_scene_comparison AB_WIDTH=3840 AB_SPP=16 bash tools/gpu_ab.sh ;;
+    ab_wf_both) rm -f gpurun_out/ab_runs.log; step ab_wf_c3 900 env AB_MODES=wf AB_REPS=3 AB_VARIANTS="${WF_VARIANTS:-}" bash tools/gpu_ab.sh &&
+      { rm -f gpurun_out/ab_runs.log; step ab_wf_fog 900 env AB_MODES=wf AB_REPS=3 AB_VARIANTS="${WF_VARIANTS:-}" AB_SCENE=cornell_mesh_fog AB_WIDTH=1024 AB_SPP=32 bash tools/gpu_ab.sh; } ;;
+    wftests) step wftests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "wf or wavefront or drain or bench_shapes or parity or edge" ;;
     parity_variants) for lib in path-tracer-python_amd/ptmi/_lib/variants/*.so; do
         step parity_$(basename $lib .so) 600 env PTMI_LIB=$PWD/$lib python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edge.py -x -q --timeout 300 --timeout-method thread; done ;;
     cache_mk|cache_wf) v=${s#cache_}; step $s 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_cache" -o $v -- python tools/ab.py $v 32 1 ;;
