@@ -93,3 +93,31 @@ def test_cpu_baseline_records_the_host_and_times_the_whole_frame():
     assert r['kind'] == 'port' and r['value'] > 0 and r['unit'] == 'Msamples/s'
     assert r['os_cpu_count'] >= r['affinity_cpus'] >= 1 and r['cores'] >= 1
     assert 'cpu_model' in r and 'the whole frame' in r['sample'] and '400x225' in r['sample']
+
+
+@pytest.mark.parametrize('preset,kernel', [('c2', 'megakernel'), ('c3', 'wf_intersect'), ('c3', 'wf_scatter'),
+                                           ('c4', 'megakernel'), ('c5', 'megakernel')])
+def test_every_preset_has_a_valu_row_from_the_same_collection(preset, kernel):
+    """The bench line's compute-side diagnostic exists for every preset's
+    dominant kernel, and every traffic and VALU row the presets read names
+    one and the same collection (the round's final kernel sources)."""
+    v = bench.valu_diagnostic(_args(['--preset', preset]), kernel)
+    assert v is not None and 0 < v['valu_issue_frac'] <= 1 and 0 < v['lane_efficiency'] <= 1
+    src = v['source'].split(' ')[0].replace('{a,b,c}', 'a')
+    assert os.path.exists(os.path.join(ROOT, src)), src
+    import re
+    heads = set()
+    for p in ('c2', 'c3', 'c4', 'c5'):
+        a = _args(['--preset', p])
+        k = 'wf_intersect' if a.variant == 'wf' else 'megakernel'
+        for s in (bench.measured_traffic(a, k)['source'], bench.valu_diagnostic(a, k)['source']):
+            heads.update(re.findall(r'HEAD ([0-9a-f]{7,})', s))
+    assert len(heads) == 1, heads
+
+
+def test_wavefront_tail_segments_are_the_drains_units():
+    """Segments the wavefront traced in its tail launch (counter [5]) are
+    wf_drain's units, not wf_intersect's."""
+    import inspect
+    src = inspect.getsource(bench.main)
+    assert "'wf_intersect': cnt['segments'] - tail" in src and "'wf_drain': tail" in src
