@@ -98,11 +98,10 @@ constexpr int kWfBlock = PTMI_WF_BLOCK;
 // LDS stacks set its occupancy: the 20-slot kernel (leaf depth 16-19, e.g.
 // the mesh-fog torus) fits 4 waves/SIMD with all slots in LDS, 7 with 11
 // (67 VGPRs). A/B on MI355X, parity-identical (also with 3 LDS slots, where
-// most pushes spill): mesh fog +2.2 %; for the 16-slot kernel (vol2, C3: 5
-// waves/SIMD) 7 waves gained nothing (-1.5 %; 6 waves -2.5 %; larger pipe
-// grids -1 to -5 %), so it keeps all 16 in LDS
-// (profiles/r03/ab/ab_wf_spill.log). A 16-slot wf_intersect padded down to 4
-// waves/SIMD loses 8 % (3 waves: 18 %).
+// most pushes spill): mesh fog +2.2 %; for the 16-slot kernel (vol2, C3) 7
+// waves measured -1.5 % on round 3's in-place slots (profiles/r03/ab/ab_wf_spill.log)
+// and +0.8 % on round 5's compacted buffers (PTMI_WF_SPILL_MIN_STACK below). A
+// 16-slot wf_intersect padded down to 4 waves/SIMD loses 8 % (3 waves: 18 %).
 #define PTMI_WF_ISECT_LDS 11
 #endif
 #ifndef PTMI_WF_SPILL_MAX_STACK
@@ -110,7 +109,13 @@ constexpr int kWfBlock = PTMI_WF_BLOCK;
 #endif
 constexpr int kSpillSlots = PTMI_WF_SPILL_MAX_STACK > PTMI_WF_ISECT_LDS ? PTMI_WF_SPILL_MAX_STACK - PTMI_WF_ISECT_LDS : 0;
 #ifndef PTMI_WF_SPILL_MIN_STACK
-#define PTMI_WF_SPILL_MIN_STACK 17  // kernels of this many stack slots up to PTMI_WF_SPILL_MAX_STACK spill
+// Kernels of this many stack slots up to PTMI_WF_SPILL_MAX_STACK spill. Round 5,
+// on the compacted buffers: the 16-slot kernel (vol2) with 11 slots in LDS and
+// 5 spilled runs at 7 waves/SIMD instead of 5: C3 +0.8 % over three A/B runs
+// (1946-1961 vs 1927-1944; 13 slots, 6 waves: -0.5 %), the mesh fog's 20-slot
+// kernel unchanged (profiles/r05/ab/ab_wf_lds_slots16.log, ab_wf_prio_block.log).
+// Round 3 had measured it -1.5 % on the in-place slots.
+#define PTMI_WF_SPILL_MIN_STACK 16
 #endif
 template <int STACK, int TRAV>
 constexpr int isect_lds() {
@@ -119,6 +124,14 @@ constexpr int isect_lds() {
              ? PTMI_WF_ISECT_LDS
              : STACK;
 }
+// Wave priority (s_setprio) of the stage kernels, which run side by side from
+// the 4 pipes: -1 = none (A/B switches).
+#ifndef PTMI_WF_PRIO_ISECT
+#define PTMI_WF_PRIO_ISECT -1
+#endif
+#ifndef PTMI_WF_PRIO_SCATTER
+#define PTMI_WF_PRIO_SCATTER -1
+#endif
 #ifndef PTMI_WF_MAX_BLOCKS
 #define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together; A/B: 4096 -1.5 %, 8192 -3.5 % (C3)
 #endif
@@ -738,6 +751,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame f
                                                        unsigned long long* __restrict__ counters) {
   constexpr int LDS = isect_lds<STACK, TRAV>();
   __shared__ uint2 lds_stack[LDS * kWfBlock];
+#if PTMI_WF_PRIO_ISECT >= 0
+  __builtin_amdgcn_s_setprio(PTMI_WF_PRIO_ISECT);
+#endif
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid, wb.spill, (uint32_t)(blockIdx.x * kWfBlock + tid) * 8u, gridDim.x * kWfBlock * 8u};
   const RayBuf& X = wb.rb[par];
@@ -1013,6 +1029,9 @@ template <int STACK, int TRAV = PTMI_TRAV_STACK>
 __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatter(DevScene sc, DevFrame fr, WfBufs wb,
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
+#if PTMI_WF_PRIO_SCATTER >= 0
+  __builtin_amdgcn_s_setprio(PTMI_WF_PRIO_SCATTER);
+#endif
   Stack st{lds_stack + threadIdx.x};
   const RayBuf& X = wb.rb[par];
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
