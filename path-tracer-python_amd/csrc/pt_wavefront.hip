@@ -1212,7 +1212,10 @@ constexpr size_t kSpillPipeBytes = (size_t)kSpillSlots * (PTMI_WF_MAX_BLOCKS / k
 Layout layout(int32_t npix, int32_t batch) {
   Layout L;
   int64_t items = (int64_t)npix * batch;
-  int64_t cap = npix > kMaxCapacity ? npix : kMaxCapacity;
+  // rays per iteration: 2^21 (or the batch's items if fewer), whatever the
+  // frame size — the pool refills the buffers, so a 4K frame needs no more
+  // (the ray buffers are 56 B x 12 positions per ray: 1.4 GB at 2^21)
+  int64_t cap = kMaxCapacity;
   if (items < cap) cap = items;
   cap = (cap + kPipes * kSlotQuantum - 1) / (kPipes * kSlotQuantum) * (kPipes * kSlotQuantum);
   L.capacity = (int32_t)cap;  // all pipes
