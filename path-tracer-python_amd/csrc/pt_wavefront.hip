@@ -516,6 +516,7 @@ __device__ __forceinline__ int32_t cont_position(const SegTable& T, const WfBufs
     return j < T.ovf_n ? ovf_base(wb) + j : -1;
   }
   const unsigned long long m = pt_ballot(lane < kBins && T.bstart <= w0 && w0 < T.bstart + T.btot);
+  if (m == 0ull) return -1;  // (a wave base never falls in a bin's padding alone: bins are padded to < 64 more)
   const int32_t b = __ffsll((long long)m) - 1;  // wave-uniform: the bin this wave reads
   const int32_t j = w0 - __builtin_amdgcn_readlane(T.bstart, b) + lane;
   if (j >= __builtin_amdgcn_readlane(T.btot, b)) return -1;
