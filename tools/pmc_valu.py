@@ -55,8 +55,9 @@ def main():
         'wave_issue_frac': round(v['SQ_ACTIVE_INST_ANY'] / v['SQ_WAVE_CYCLES'], 4),
         'valu_insts': v['SQ_INSTS_VALU'],
         'kernel_ms': round(cycles / 2.4e6, 3),
-        'source': os.path.relpath(d, ROOT) + f'/{prefix}_{{a,b,c}}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
-                  f'tools/ab.py {prefix} 32 1, one 32-spp call; kernel {kern}); tools/pmc_valu.py',
+        'source': os.environ.get('PMC_SOURCE') or (
+            os.path.relpath(d, ROOT) + f'/{prefix}_{{a,b,c}}_counter_collection.csv (tools/gpu_pmc_latency.sh: '
+            f'tools/ab.py {prefix} 32 1, one 32-spp call; kernel {kern}); tools/pmc_valu.py'),
     }
     path = os.path.join(ROOT, 'profiles', 'valu.json')
     rows = {}
