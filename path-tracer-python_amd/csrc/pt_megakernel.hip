@@ -74,10 +74,35 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // next node load goes out sooner (A/B with SHADE_AT 12: C2 +1.3 %, C4 +4 %,
 // C5 +1.4 %; the reverse order -1 %; profiles/r01/ab_prio_shade_at.log).
 // -1 = no s_setprio.
-#define PTMI_MK_PRIO_TRAV 1
+#define PTMI_MK_PRIO_TRAV 2
 #endif
 #ifndef PTMI_MK_PRIO_SHADE
-#define PTMI_MK_PRIO_SHADE 0
+#define PTMI_MK_PRIO_SHADE 1
+#endif
+#ifndef PTMI_MK_PRIO_DRAIN
+// Traversal priority of a persistent wave whose units have run out: its
+// drain, the longest of its remaining paths, runs with ~21 % of its lanes
+// live and issues every instruction for them (probe, tools/drain_probe.py:
+// 12 % of the waves' cycles in an 8-GPU tile shard's 5 M-sample call, 1.7 %
+// in a whole-frame 64-spp call). Below shading and every fuller wave's
+// traversal, it takes the issue cycles they leave. A/B on MI355X
+// (parity-identical; traversal 2 / shading 1 / drain 0 against 1 / 0 / 1):
+// C2 +2 %, C4 +2 %, whole frame at 64 spp per call +2.9 %, an 8-rank tile
+// shard +2.7 %; drain 0 with traversal 1 / shading 0: +1.7 %, C4 -0.6 %
+// (profiles/r05/ab/ab_mk_prio_drain.log). Handing the drained waves' paths
+// to a second launch instead (full waves, the rest of the chip free) lost 2
+// to 8 %: that launch waits behind the next overlapped call's persistent
+// waves (profiles/r05/ab/ab_mk_handover.log). -1: PTMI_MK_PRIO_TRAV.
+#define PTMI_MK_PRIO_DRAIN 0
+#endif
+#ifndef PTMI_MK_PRIO_DRAIN_SHADE
+#define PTMI_MK_PRIO_DRAIN_SHADE -1  // shading priority of a draining wave (-1: PTMI_MK_PRIO_SHADE)
+#endif
+#ifndef PTMI_MK_PRIO_FULL
+#define PTMI_MK_PRIO_FULL -1  // traversal priority of a wave with >= PTMI_MK_PRIO_FULL_AT busy lanes (-1: off)
+#endif
+#ifndef PTMI_MK_PRIO_FULL_AT
+#define PTMI_MK_PRIO_FULL_AT 48
 #endif
 // A/B, not kept (profiles/): Perlin-textured hits held until 4 or 8 of a wave
 // are ready, -1 to -1.5 % (r01/ab_mk_hold_noise.log); non-temporal staging
@@ -330,6 +355,14 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   };
   if (live) begin_segment();
 
+#if PTMI_PROBE == 3
+  // drain probe (diagnostic build, tools/drain_probe.py): a persistent wave's
+  // cycles, its cycles after the batch's units ran out for it, and live-lane x
+  // cycles in them
+  const uint64_t dr_t0 = __builtin_amdgcn_s_memtime();
+  uint64_t dr_tdry = 0, dr_prev = 0, dr_lanecyc = 0;
+  bool dr_dry = false;
+#endif
 #if PTMI_PROBE == 2
   // wave-level probe (diagnostic build): shader cycles in the traversal-step
   // loop and in shading/refill; wave steps and the branches they ran
@@ -338,7 +371,12 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #endif
   for (;;) {
 #if PTMI_MK_PRIO_TRAV >= 0
-    __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
+#if PTMI_MK_PRIO_DRAIN >= 0
+    if (kPersist && drained && next >= wend)  // a draining wave: its few live lanes yield issue to full waves
+      __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_DRAIN);
+    else
+#endif
+      __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
 #endif
     for (;;) {  // traversal steps
       // a lane's stack is empty unless its segment is mid-traversal (busy => trav)
@@ -347,6 +385,14 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
       if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
+#if PTMI_MK_PRIO_FULL >= 0 && PTMI_MK_PRIO_TRAV >= 0
+      if (!(kPersist && drained && next >= wend)) {
+        if (nbusy >= (uint32_t)PTMI_MK_PRIO_FULL_AT)
+          __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_FULL);
+        else
+          __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
+      }
+#endif
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -372,7 +418,12 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     }
 #endif
 #if PTMI_MK_PRIO_TRAV >= 0
-    __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
+#if PTMI_MK_PRIO_DRAIN >= 0 && PTMI_MK_PRIO_DRAIN_SHADE >= 0
+    if (kPersist && drained && next >= wend)
+      __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_DRAIN_SHADE);
+    else
+#endif
+      __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
     const bool shade_now = trav && !tr.busy();
 #if PTMI_MK_WAVE_TURB
@@ -587,6 +638,18 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
         pr_t = t;
       }
 #endif
+#if PTMI_PROBE == 3
+      if (drained && next >= wend) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (!dr_dry) {
+          dr_dry = true;
+          dr_tdry = t;
+        } else {
+          dr_lanecyc += (t - dr_prev) * (uint64_t)__popcll(__ballot(live || trav));
+        }
+        dr_prev = t;
+      }
+#endif
       if (__ballot(live) == 0ull && drained && next >= wend) break;
     } else {
       if (need_seg) {
@@ -596,6 +659,15 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       if (__ballot(live) == 0ull) break;
     }
   }
+#if PTMI_PROBE == 3
+  if (kPersist && lane == 0) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    atomicAdd(&g_probe[0], t - dr_t0);
+    atomicAdd(&g_probe[1], dr_dry ? t - dr_tdry : 0ull);
+    atomicAdd(&g_probe[2], dr_lanecyc);
+    atomicAdd(&g_probe[3], 1ull);
+  }
+#endif
 #if PTMI_PROBE == 2
   if (lane == 0) {
     atomicAdd(&g_probe[8], pr_trav);

@@ -24,6 +24,8 @@
 #   abpmc_<lib>_<mk|wf>   FETCH_SIZE, WRITE_SIZE and cache-hit PMC passes of tools/ab.py (32 spp x 1), same libs
 #   ablat_<lib>_<mk|wf>   the VALU / wait PMC passes (tools/gpu_pmc_latency.sh) with variants/libptmi_<lib>.so
 #   probe                 the diagnostic probe builds (tools/gpu_probe.sh; variants libptmi_probe{1,2}.so)
+#   callsize              tools/call_size.py (whole frame at 64 / 8 spp per call, an 8-rank tile shard at 64)
+#                         for the default build and every variants/*.so (MK_VARIANTS: only those), two rounds
 # Every step has its own time limit; the script stops at the first failure.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -64,6 +66,12 @@ for s in $STEPS; do
     latc4_mk|latc4_wf) v=${s#latc4_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_c4_$v PMC_SCENE_ARGS="cornell_mesh_fog 1024" bash tools/gpu_pmc_latency.sh ;;
     latc5_mk) step $s 600 env PMC_VARIANT=mk PMC_DIR=$OUT/pmc_latency_c5_mk PMC_SCENE_ARGS="vol2_final_scene_comparison 3840" bash tools/gpu_pmc_latency.sh ;;
     probe) step probe 600 bash tools/gpu_probe.sh ;;
+    callsize) libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so)
+      if [ -n "${MK_VARIANTS:-}" ]; then for n in $MK_VARIANTS; do libs+=(path-tracer-python_amd/ptmi/_lib/variants/libptmi_$n.so); done
+      else libs+=(path-tracer-python_amd/ptmi/_lib/variants/*.so); fi
+      for r in 1 2; do for lib in "${libs[@]}"; do
+        PTMI_LIB=$PWD/$lib CALL_SIZE_SPP=64,8 CALL_SIZE_SHARDS=8:4 step callsize_$(basename $lib .so)_$r 300 python tools/call_size.py
+        cat "$OUT/callsize_$(basename $lib .so)_$r.log" | grep full_ | sed "s/^/$(basename $lib .so) /" >> "$OUT/callsize.txt"; done; done ;;
     abtrace_*) r=${s#abtrace_}; name=${r%_*}; mode=${r##*_}
       lib=path-tracer-python_amd/ptmi/_lib/libptmi.so; [ "$name" = default ] || lib=path-tracer-python_amd/ptmi/_lib/variants/libptmi_$name.so
       PTMI_LIB=$PWD/$lib step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/abtrace" -o ${name}_$mode -- python tools/ab.py $mode 64 2 ${AB_SCENE:-vol2_final_scene} ${AB_WIDTH:-800} ;;
