@@ -195,15 +195,17 @@ class Integrator:
     # (profiles/r03/ab/ab_staging_bytes.log).
     STAGING_BYTES = int(os.environ.get('PTMI_STAGING_BYTES', str(2 << 30)))
     # Overlapped megakernel calls: traces in flight, one workspace and side
-    # stream each. Two for full-frame calls; three for small calls, whose
-    # drain is a larger part of a launch. A/B on MI355X (vol2 800x800, 64 spp
-    # per call): the full frame (41 M samples per call) 2851 (2) vs 2762 (3)
-    # Msamples/s; an 8-GPU tile shard (5.1 M samples per call, rehearsed on one
-    # GPU, tools/shard_balance.py) 2380-2487 (2) vs 2450-2565 (3) per GPU; 4
-    # in flight is slower than both (profiles/r03/overlap_depth_and_bands.log).
+    # stream each. Round 3 measured two in flight for whole-frame calls and
+    # three for small calls (vol2 800x800, 64 spp per call: the full frame,
+    # 41 M samples per call, 2851 (2) vs 2762 (3) Msamples/s; an 8-GPU tile
+    # shard, 5.1 M samples per call, 2380-2487 (2) vs 2450-2565 (3); 4 slower
+    # than both; profiles/r03/overlap_depth_and_bands.log). Since draining
+    # waves traverse at the lowest priority (pt_megakernel.hip,
+    # PTMI_MK_PRIO_DRAIN) three are as fast on whole frames too: C2 3314 vs
+    # 3312, C5 4306 vs 4314, C4 1786 vs 1760; the shard 3085 (3) vs 2985 (2)
+    # vs 3092 (4) (profiles/r05/overlap_depth_r05.log), so three always.
     # PTMI_OVERLAP_DEPTH fixes the depth (A/B only).
     OVERLAP_DEPTH_MAX = 3
-    OVERLAP_SMALL_CALL = 8_000_000  # samples per call below which 3 traces overlap
 
     def render_mk_overlapped(self, frame, accum, sample_begin, sample_count, stream=None):
         """Megakernel calls whose launches overlap: each batch is traced
@@ -247,8 +249,7 @@ class Integrator:
                     for side in self._ov['streams']:
                         side.wait_event(self._reset_event)
             ov = self._ov
-            depth = int(os.environ.get('PTMI_OVERLAP_DEPTH', '0')) or \
-                (3 if npix * min(per, int(sample_count)) < self.OVERLAP_SMALL_CALL else 2)
+            depth = int(os.environ.get('PTMI_OVERLAP_DEPTH', '0')) or self.OVERLAP_DEPTH_MAX
             depth = max(1, min(depth, len(ov['ws'])))
             b = 0
             while b < sample_count:
