@@ -24,6 +24,8 @@
 #   abpmc_<lib>_<mk|wf>   FETCH_SIZE, WRITE_SIZE and cache-hit PMC passes of tools/ab.py (32 spp x 1), same libs
 #   ablat_<lib>_<mk|wf>   the VALU / wait PMC passes (tools/gpu_pmc_latency.sh) with variants/libptmi_<lib>.so
 #   probe                 the diagnostic probe builds (tools/gpu_probe.sh; variants libptmi_probe{1,2}.so)
+#   abbench_<c>           bench.py --preset <c> (no CPU baseline) for the default build and every variants/*.so
+#                         (MK_VARIANTS: only those), two interleaved rounds -> OUT/abbench_<c>.txt
 #   callsize              tools/call_size.py (whole frame at 64 / 8 spp per call, an 8-rank tile shard at 64)
 #                         for the default build and every variants/*.so (MK_VARIANTS: only those), two rounds
 # Every step has its own time limit; the script stops at the first failure.
@@ -66,6 +68,12 @@ for s in $STEPS; do
     latc4_mk|latc4_wf) v=${s#latc4_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_c4_$v PMC_SCENE_ARGS="cornell_mesh_fog 1024" bash tools/gpu_pmc_latency.sh ;;
     latc5_mk) step $s 600 env PMC_VARIANT=mk PMC_DIR=$OUT/pmc_latency_c5_mk PMC_SCENE_ARGS="vol2_final_scene_comparison 3840" bash tools/gpu_pmc_latency.sh ;;
     probe) step probe 600 bash tools/gpu_probe.sh ;;
+    abbench_*) c=${s#abbench_}; libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so)
+      if [ -n "${MK_VARIANTS:-}" ]; then for n in $MK_VARIANTS; do libs+=(path-tracer-python_amd/ptmi/_lib/variants/libptmi_$n.so); done
+      else libs+=(path-tracer-python_amd/ptmi/_lib/variants/*.so); fi
+      for r in 1 2; do for lib in "${libs[@]}"; do n=$(basename $lib .so)
+        PTMI_LIB=$PWD/$lib step abbench_${c}_${n}_$r 300 python bench.py --preset $c --no-cpu-baseline
+        echo "$n $(grep -o '"value": [0-9.]*' "$OUT/abbench_${c}_${n}_$r.log" | head -1)" >> "$OUT/abbench_$c.txt"; done; done ;;
     callsize) libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so)
       if [ -n "${MK_VARIANTS:-}" ]; then for n in $MK_VARIANTS; do libs+=(path-tracer-python_amd/ptmi/_lib/variants/libptmi_$n.so); done
       else libs+=(path-tracer-python_amd/ptmi/_lib/variants/*.so); fi
