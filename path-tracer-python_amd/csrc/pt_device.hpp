@@ -257,6 +257,10 @@ __device__ __forceinline__ bool pt_all2(bool a, bool b) {
 // Sphere roots (h -+ sqrt(disc)) / a through a per-ray reciprocal of a
 // (pt_div_by, include/ptmi_math.h): A/B on MI355X, parity-identical: C2 +0.9 %, C5 +0.6 %, C3
 // +0.3 % (profiles/r02/ab/ab_sphere_markstein.log)
+// EXCL: the caller updates the closest hit only when t < tmax (tmax being
+// the current closest t), so the final range test takes t < tmax itself and
+// the caller drops its compare: the same updates, one compare fewer.
+template <bool EXCL = false>
 __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, float tmin, float tmax,
                                              float& t) {  // kernels.py:209-248
   pt_v3 c = pt_v3f(s.x, s.y, s.z);
@@ -271,19 +275,20 @@ __device__ __forceinline__ bool hit_sphere_t(const float4 s, pt_v3 o, pt_v3 d, f
     float sq = sqrtf(disc);
     float root = PT_SPH_DIV(h - sq);
     if (root < tmin || root > tmax) root = PT_SPH_DIV(h + sq);
-    if (pt_all2(root >= tmin, root <= tmax)) { t = root; return true; }
+    if (pt_all2(root >= tmin, EXCL ? root < tmax : root <= tmax)) { t = root; return true; }
   }
   return false;
 #undef PT_SPH_DIV
 }
 
+template <bool EXCL = false>
 __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const float4 c, const float4 e, pt_v3 o,
                                            pt_v3 d, float tmin, float tmax, float& t) {  // kernels.py:311-362
   pt_v3 n = pt_v3f(a.x, a.y, a.z);
   float denom = pt_dot(n, d);
   if (fabsf(denom) >= 1e-8f) {
     float tt = (a.w - pt_dot(n, o)) / denom;
-    if (pt_all2(tt >= tmin, tt <= tmax)) {
+    if (pt_all2(tt >= tmin, EXCL ? tt < tmax : tt <= tmax)) {
       pt_v3 Q = pt_v3f(b.x, b.y, b.z), u = pt_v3f(b.w, c.x, c.y), v = pt_v3f(c.z, c.w, e.x);
       pt_v3 w = pt_v3f(e.y, e.z, e.w);
       pt_v3 ip = pt_add(o, pt_scale(d, tt));
@@ -296,6 +301,7 @@ __device__ __forceinline__ bool hit_quad_v(const float4 a, const float4 b, const
   return false;
 }
 
+template <bool EXCL = false>
 __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o, pt_v3 d, float tmin,
                                            float tmax, float& t) {
   // all 64 B in one round trip (the compiler otherwise sinks the loads into
@@ -303,10 +309,11 @@ __device__ __forceinline__ bool hit_quad_t(const float4* __restrict__ q, pt_v3 o
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
   pt_f4 A = ((const pt_f4*)q)[0], B = ((const pt_f4*)q)[1], C = ((const pt_f4*)q)[2], E = ((const pt_f4*)q)[3];
   asm volatile("" : "+v"(A), "+v"(B), "+v"(C), "+v"(E));
-  return hit_quad_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
+  return hit_quad_v<EXCL>(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
                     make_float4(C.x, C.y, C.z, C.w), make_float4(E.x, E.y, E.z, E.w), o, d, tmin, tmax, t);
 }
 
+template <bool EXCL = false>
 __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const float4 c, pt_v3 o, pt_v3 d,
                                           float tmin, float tmax, float& t) {  // kernels.py:252-307
   pt_v3 v0 = pt_v3f(a.x, a.y, a.z), e1 = pt_v3f(a.w, b.x, b.y), e2 = pt_v3f(b.z, b.w, c.x);
@@ -321,7 +328,7 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
       float v = inv * pt_dot(d, q);
       if (pt_all2(v >= 0.0f, u + v <= 1.0f)) {
         float tt = inv * pt_dot(e2, q);
-        if (pt_all2(tt >= tmin, tt <= tmax)) { t = tt; return true; }
+        if (pt_all2(tt >= tmin, EXCL ? tt < tmax : tt <= tmax)) { t = tt; return true; }
       }
     }
   }
@@ -331,6 +338,7 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
 #ifndef PTMI_TRI_E2Z_DWORD
 #define PTMI_TRI_E2Z_DWORD 0
 #endif
+template <bool EXCL = false>
 __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
                                           float tmax, float& t) {
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
@@ -339,13 +347,13 @@ __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o
   // the test reads e2.z of the third 16 B only (the normal is read at shading)
   float cx = ((const float*)tr)[8];
   asm volatile("" : "+v"(A), "+v"(B), "+v"(cx));
-  return hit_tri_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w), make_float4(cx, 0.0f, 0.0f, 0.0f),
+  return hit_tri_v<EXCL>(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w), make_float4(cx, 0.0f, 0.0f, 0.0f),
                    o, d, tmin, tmax, t);
 #else
   pt_f4 C = ((const pt_f4*)tr)[2];
   asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
-  return hit_tri_v(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
-                   make_float4(C.x, C.y, C.z, C.w), o, d, tmin, tmax, t);
+  return hit_tri_v<EXCL>(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
+                         make_float4(C.x, C.y, C.z, C.w), o, d, tmin, tmax, t);
 #endif
 }
 
@@ -502,6 +510,19 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 // re-issues its own v_cmp): 2 VALU fewer per pop. A/B on MI355X
 // (parity-identical, GPU suite green): C2 +1.8 %, C4 +1.4 %, C5 +1.8 %, mesh
 // fog wavefront +0.8 %, C3 +-0 (profiles/r05/ab/ab_step_masks.log).
+// The leaf test of a pop with the closest-hit update inside each primitive's
+// branch (no hit flag or t merged across the three branches: 35 SALU fewer
+// per pop, 20 VALU more in the code, mostly in branches a pop skips), and its
+// range test with t < closest itself (EXCL: the caller's compare dropped).
+// A/B on MI355X (parity-identical): C2 +0.4 %, C4 +1.3 %, C5 +0.5 %, C3 +1 %,
+// mesh fog +1 % (update alone: +0.3 / +1.2 / +0.3 / +0.5 / +0.6 %;
+// profiles/r05/ab/ab_leaf_update.log).
+#ifndef PTMI_LEAF_UPDATE
+#define PTMI_LEAF_UPDATE 1
+#endif
+#ifndef PTMI_LEAF_EXCL
+#define PTMI_LEAF_EXCL 1
+#endif
 #ifndef PTMI_STEP_MASKS
 #define PTMI_STEP_MASKS 1
 #endif
@@ -641,10 +662,33 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     tr.probe |= leaf_type(ref) == kSphere ? 1 : 2;
 #endif
     float t;  // leaf: kernels.py:671-697
+#if PTMI_LEAF_UPDATE
+    // each primitive branch updates the closest hit itself: no hit flag or t
+    // merged across the three branches
+    const int32_t ty = leaf_type(ref), ix = leaf_index(ref);
+    constexpr bool kX = PTMI_LEAF_EXCL != 0;  // the range test takes t < closest (hit_sphere_t)
+    if (ty == kSphere) {
+      if (hit_sphere_t<kX>(sc.spheres[ix], o, d, tr.tmin, tr.closest, t) && (kX || t < tr.closest)) {
+        tr.closest = t;
+        tr.best = ref;
+      }
+    } else if (ty == kQuad) {
+      if (hit_quad_t<kX>(sc.quads + 4 * ix, o, d, tr.tmin, tr.closest, t) && (kX || t < tr.closest)) {
+        tr.closest = t;
+        tr.best = ref;
+      }
+    } else {
+      if (hit_tri_t<kX>(sc.tris + 3 * ix, o, d, tr.tmin, tr.closest, t) && (kX || t < tr.closest)) {
+        tr.closest = t;
+        tr.best = ref;
+      }
+    }
+#else
     if (hit_leaf(sc, ref, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
       tr.closest = t;
       tr.best = ref;
     }
+#endif
     return;
   }
 #if PTMI_PROBE == 2
