@@ -517,6 +517,15 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 // A/B on MI355X (parity-identical): C2 +0.4 %, C4 +1.3 %, C5 +0.5 %, C3 +1 %,
 // mesh fog +1 % (update alone: +0.3 / +1.2 / +0.3 / +0.5 / +0.6 %;
 // profiles/r05/ab/ab_leaf_update.log).
+// ... and the deferred lanes as a third mask: they restore their pointer
+// with one select in a scalar branch taken only when some lane defers, the
+// others branch once on live & ~deferred (one level of nesting, ~3 SALU, fewer
+// per pop). A/B on MI355X (parity-identical): C2 +1.0 %, C4 +1.4 %, C5 +1.0 %;
+// with the step loop's first pop reading the header's busy mask
+// (PTMI_MK_HDR_REUSE) +1.2 / +1.4 / +1.0 % (profiles/r05/ab/ab_step_flat.log).
+#ifndef PTMI_STEP_FLAT
+#define PTMI_STEP_FLAT 1
+#endif
 #ifndef PTMI_LEAF_UPDATE
 #define PTMI_LEAF_UPDATE 1
 #endif
@@ -624,6 +633,19 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   // and the leaf/node branch all read them
   const unsigned long long m_leaf = pt_ballot(ref < 0), m_live = pt_ballot(__uint_as_float(ent.y) <= tr.closest);
 #endif
+#if PTMI_STEP_MASKS && PTMI_STEP_FLAT
+  unsigned long long m_go = m_live;  // lanes that test their popped entry in this step
+  if constexpr (DEFER > 0) {
+    // the deferred lanes as one more mask: they restore their pointer, the
+    // rest branch once on m_go (one level of nesting fewer)
+    const unsigned long long md = m_leaf & m_live;
+    const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
+    const unsigned long long mdef = (md != 0ull && md != pt_ballot(true) && nd < (uint32_t)DEFER) ? md : 0ull;
+    if (mdef != 0ull) tr.sp += __builtin_amdgcn_inverse_ballot_w64(mdef) ? kSlot : 0u;
+    m_go &= ~mdef;
+  }
+  if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
+#else
   if constexpr (DEFER > 0) {
 #if PTMI_STEP_MASKS
     const unsigned long long md = m_leaf & m_live;
@@ -651,8 +673,11 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
 #endif
 #endif
+#endif
 #if PTMI_STEP_MASKS
+#if !PTMI_STEP_FLAT
   if (!__builtin_amdgcn_inverse_ballot_w64(m_live)) return;
+#endif
   if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {
 #else
   if (!(__uint_as_float(ent.y) <= tr.closest)) return;
