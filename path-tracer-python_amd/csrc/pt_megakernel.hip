@@ -359,6 +359,20 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
   };
   if (live) begin_segment();
 
+#if PTMI_PROBE == 4
+  // shading-round probe (diagnostic build, tools/probe.py --sections): wave
+  // cycles per section of the outer loop
+  uint64_t p4[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t p4_t = __builtin_amdgcn_s_memtime();
+#define PT_P4(k)                                        \
+  {                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    p4[k] += t_ - p4_t;                                 \
+    p4_t = t_;                                          \
+  }
+#else
+#define PT_P4(k)
+#endif
 #if PTMI_PROBE == 3
   // drain probe (diagnostic build, tools/drain_probe.py): a persistent wave's
   // cycles, its cycles after the batch's units ran out for it, and live-lane x
@@ -435,6 +449,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
 #endif
       __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
+    PT_P4(0)  // traversal steps
     const bool shade_now = trav && !tr.busy();
 #if PTMI_MK_WAVE_TURB
     // Perlin-textured surface hits of this round: their turbulence by the
@@ -453,6 +468,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     pt_v3 hp = pt_v3f(0.0f, 0.0f, 0.0f), sdir = hp, att = hp, n = hp;
     int32_t ruv = kRuvNone, sref = 0;
     float4 m0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the metal's albedo and fuzz (scatter_end)
+    PT_P4(1)  // wave turbulence
     if (shade_now) {  // segment traced: shade it
       trav = false;
       const bool exit_mode = ps.mode == kModeMediumExit;
@@ -511,6 +527,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
         }
       }
     }
+    PT_P4(2)  // material, medium step, surface scatter (first half)
     // one random_unit_vector site per round: medium, metal fuzz, isotropic
 #if PTMI_MK_WAVE_RUV
     if (pt_ballot(ruv != kRuvNone) != 0ull) {
@@ -536,6 +553,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       }
     }
 #endif
+    PT_P4(3)  // unit vector (wave) and scatter_end
     if (shade_now) {
       if (!done && !to_medium) {
         if (scattered) {  // kernels.py:1131-1157
@@ -588,6 +606,7 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
         need_seg = true;  // next segment of this path (or its medium exit search)
       }
     }
+    PT_P4(4)  // epilogue: RR, staging
     if (kPersist) {  // hand the wave's next items to the lanes without a path, fetching units as needed
       const unsigned long long want = __ballot(!live);
       if (want && !(drained && next >= wend)) {
@@ -637,10 +656,12 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
           }
         }
       }
+      PT_P4(5)  // refill: unit fetch, bind, camera ray
       if (need_seg) {
         need_seg = false;
         begin_segment();
       }
+      PT_P4(6)  // segment begin (inverse direction, root slab)
 #if PTMI_PROBE == 2
       {
         const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -669,6 +690,11 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       if (__ballot(live) == 0ull) break;
     }
   }
+#if PTMI_PROBE == 4
+  if (kPersist && lane == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_probe[k], p4[k]);
+#endif
+#undef PT_P4
 #if PTMI_PROBE == 3
   if (kPersist && lane == 0) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
