@@ -497,55 +497,6 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 #ifndef PTMI_PROBE
 #define PTMI_PROBE 0
 #endif
-// Leaf deferral's ballot from the two compares' lane masks (s_and) instead of
-// their && materialised with v_cndmask + v_cmp: 2 VALU fewer per pop. A/B on
-// MI355X (parity-identical): C2 +1.0 %, C4 +0.6 %, C5 +0.9 %; the same
-// rewrite of the step loop's shading test as well: +0.4 % / +0.4 % / +0.3 %
-// (profiles/r05/ab/ab_mk_defer_masks.log). 0: the && form.
-#ifndef PTMI_DEFER_MASKS
-#define PTMI_DEFER_MASKS 1
-#endif
-// ... and the pop's two tests (leaf?, live?) as lane masks computed once and
-// read by the deferral, the cull and the leaf/node branch (each otherwise
-// re-issues its own v_cmp): 2 VALU fewer per pop. A/B on MI355X
-// (parity-identical, GPU suite green): C2 +1.8 %, C4 +1.4 %, C5 +1.8 %, mesh
-// fog wavefront +0.8 %, C3 +-0 (profiles/r05/ab/ab_step_masks.log).
-// The leaf test of a pop with the closest-hit update inside each primitive's
-// branch (no hit flag or t merged across the three branches: 35 SALU fewer
-// per pop, 20 VALU more in the code, mostly in branches a pop skips), and its
-// range test with t < closest itself (EXCL: the caller's compare dropped).
-// A/B on MI355X (parity-identical): C2 +0.4 %, C4 +1.3 %, C5 +0.5 %, C3 +1 %,
-// mesh fog +1 % (update alone: +0.3 / +1.2 / +0.3 / +0.5 / +0.6 %;
-// profiles/r05/ab/ab_leaf_update.log).
-// ... and the deferred lanes as a third mask: they restore their pointer
-// with one select in a scalar branch taken only when some lane defers, the
-// others branch once on live & ~deferred (one level of nesting, ~3 SALU, fewer
-// per pop). A/B on MI355X (parity-identical): C2 +1.0 %, C4 +1.4 %, C5 +1.0 %;
-// with the step loop's first pop reading the header's busy mask
-// (PTMI_MK_HDR_REUSE) +1.2 / +1.4 / +1.0 % (profiles/r05/ab/ab_step_flat.log).
-#ifndef PTMI_STEP_FLAT
-#define PTMI_STEP_FLAT 1
-#endif
-#ifndef PTMI_LEAF_UPDATE
-#define PTMI_LEAF_UPDATE 1
-#endif
-#ifndef PTMI_LEAF_EXCL
-#define PTMI_LEAF_EXCL 1
-#endif
-// ... and (TC) the three branches leaving only their candidate t, one
-// compare after them, with (IFS) independent branches on the type's lane
-// masks instead of an if / else chain: 48 VALU and 50 SALU fewer in the loop.
-// A/B on MI355X (parity-identical): C2 +0.45 %, C4 +0.45 %, C5 +0.5 %, C3
-// +0.5 %, mesh fog +0.8 %; TC alone -0.3 % (profiles/r05/ab/ab_leaf_tc.log).
-#ifndef PTMI_LEAF_TC
-#define PTMI_LEAF_TC 1
-#endif
-#ifndef PTMI_LEAF_IFS
-#define PTMI_LEAF_IFS 1
-#endif
-#ifndef PTMI_STEP_MASKS
-#define PTMI_STEP_MASKS 1
-#endif
 #if PTMI_PROBE
 __device__ unsigned long long g_probe[16];
 #endif
@@ -639,76 +590,48 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   tr.sp -= kSlot;
   const pt_u2v ent = stack_load<STACK, LDS, SB>(st, lim, tr.sp);
   const int32_t ref = (int32_t)ent.x;
-#if PTMI_STEP_MASKS
-  // the pop's two tests as lane masks, computed once: the deferral, the cull
-  // and the leaf/node branch all read them
+  // The pop's tests as lane masks, each computed once (round 5): leaf? and
+  // live? (E <= closest), and with DEFER the deferred lanes; the cull, the
+  // leaf / node branch and the deferral read the masks instead of re-issuing
+  // compares, the non-deferred live lanes branch once, a deferred lane
+  // restores its pointer by one select in a scalar branch taken only when some
+  // lane defers. In the leaf branch the three primitive tests are independent
+  // branches on the type's lane masks, each leaving its candidate t (one
+  // register across them), and one compare after them updates the closest
+  // hit (the tests take t < closest themselves, hit_*_t<true>). A/B on MI355X
+  // (parity-identical, each against the step before it; profiles/r05/ab/):
+  // deferral ballot from masks (no && materialised with v_cndmask + v_cmp)
+  // C2 +1.0 %, C4 +0.6 %, C5 +0.9 % (ab_mk_defer_masks.log); the masks shared
+  // by the cull and the branch C2 +1.8 %, C4 +1.4 %, C5 +1.8 %, mesh fog
+  // wavefront +0.8 % (ab_step_masks.log); the closest-hit update inside each
+  // type's branch with t < closest in the test +0.4 / +1.3 / +0.5 %, C3 +1 %
+  // (ab_leaf_update.log); the deferred lanes as a mask and one branch level
+  // fewer +1.0 / +1.4 / +1.0 % (ab_step_flat.log); independent type branches
+  // with a candidate t +0.45 / +0.45 / +0.5 %, C3 +0.5 % (ab_leaf_tc.log).
   const unsigned long long m_leaf = pt_ballot(ref < 0), m_live = pt_ballot(__uint_as_float(ent.y) <= tr.closest);
-#endif
-#if PTMI_STEP_MASKS && PTMI_STEP_FLAT
-  unsigned long long m_go = m_live;  // lanes that test their popped entry in this step
+  unsigned long long m_def = 0ull;  // deferred lanes
   if constexpr (DEFER > 0) {
-    // the deferred lanes as one more mask: they restore their pointer, the
-    // rest branch once on m_go (one level of nesting fewer)
     const unsigned long long md = m_leaf & m_live;
     const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
-    const unsigned long long mdef = (md != 0ull && md != pt_ballot(true) && nd < (uint32_t)DEFER) ? md : 0ull;
-    if (mdef != 0ull) tr.sp += __builtin_amdgcn_inverse_ballot_w64(mdef) ? kSlot : 0u;
-    m_go &= ~mdef;
+    m_def = (md != 0ull && md != pt_ballot(true) && nd < (uint32_t)DEFER) ? md : 0ull;
+    if (m_def != 0ull) tr.sp += __builtin_amdgcn_inverse_ballot_w64(m_def) ? kSlot : 0u;  // kept on top
   }
-  if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
-#else
-  if constexpr (DEFER > 0) {
-#if PTMI_STEP_MASKS
-    const unsigned long long md = m_leaf & m_live;
-    const bool dl = __builtin_amdgcn_inverse_ballot_w64(md);
-#elif PTMI_DEFER_MASKS
-    // the two compares straight into lane masks (a && b would be materialised
-    // with v_cndmask + v_cmp before the ballot)
-    const unsigned long long md = pt_ballot(ref < 0) & pt_ballot(__uint_as_float(ent.y) <= tr.closest);
-    const bool dl = __builtin_amdgcn_inverse_ballot_w64(md);
-#else
-    const bool dl = ref < 0 && __uint_as_float(ent.y) <= tr.closest;
-    const unsigned long long md = pt_ballot(dl);
-#endif
-    const unsigned long long mact = pt_ballot(true);
-    const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
-    if (md != 0ull && md != mact && nd < (uint32_t)DEFER && dl) {
-      tr.sp += kSlot;  // kept on top: popped in a later step
-      return;
-    }
-  }
-#if PTMI_PROBE
+  const unsigned long long m_go = m_live & ~m_def;  // lanes that test their popped entry in this step
 #if PTMI_PROBE == 1
-  atomicAdd(&g_probe[4], 1ull);                                                    // pops
-  if (!(__uint_as_float(ent.y) <= tr.closest)) atomicAdd(&g_probe[5], 1ull);       // culled pops
-  else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
+  if (!__builtin_amdgcn_inverse_ballot_w64(m_def)) {
+    atomicAdd(&g_probe[4], 1ull);                                                        // pops
+    if (!__builtin_amdgcn_inverse_ballot_w64(m_live)) atomicAdd(&g_probe[5], 1ull);      // culled pops
+    else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
+  }
 #endif
-#endif
-#endif
-#if PTMI_STEP_MASKS
-#if !PTMI_STEP_FLAT
-  if (!__builtin_amdgcn_inverse_ballot_w64(m_live)) return;
-#endif
-  if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {
-#else
-  if (!(__uint_as_float(ent.y) <= tr.closest)) return;
-  if (ref < 0) {
-#endif
+  if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
+  if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {  // leaf: kernels.py:671-697
 #if PTMI_PROBE == 2
     tr.probe |= leaf_type(ref) == kSphere ? 1 : 2;
 #endif
-    float t;  // leaf: kernels.py:671-697
-#if PTMI_LEAF_UPDATE
-    // each primitive branch updates the closest hit itself: no hit flag or t
-    // merged across the three branches
+    float t;
     const int32_t ty = leaf_type(ref), ix = leaf_index(ref);
-    constexpr bool kX = PTMI_LEAF_EXCL != 0;  // the range test takes t < closest (hit_sphere_t)
-#if PTMI_LEAF_TC
-    // the branches leave only their candidate t (one register across them);
-    // a hit has t < closest (EXCL), so one compare after them decides
     float tc = tr.closest;
-#if PTMI_LEAF_IFS
-    // three independent branches on the type's lane masks (no if / else chain)
     const unsigned long long m_s = pt_ballot(ty == kSphere), m_q = pt_ballot(ty == kQuad);
     if (__builtin_amdgcn_inverse_ballot_w64(m_s)) {
       if (hit_sphere_t<true>(sc.spheres[ix], o, d, tr.tmin, tr.closest, t)) tc = t;
@@ -719,43 +642,10 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     if (__builtin_amdgcn_inverse_ballot_w64(~(m_s | m_q))) {
       if (hit_tri_t<true>(sc.tris + 3 * ix, o, d, tr.tmin, tr.closest, t)) tc = t;
     }
-#else
-    if (ty == kSphere) {
-      if (hit_sphere_t<true>(sc.spheres[ix], o, d, tr.tmin, tr.closest, t)) tc = t;
-    } else if (ty == kQuad) {
-      if (hit_quad_t<true>(sc.quads + 4 * ix, o, d, tr.tmin, tr.closest, t)) tc = t;
-    } else {
-      if (hit_tri_t<true>(sc.tris + 3 * ix, o, d, tr.tmin, tr.closest, t)) tc = t;
-    }
-#endif
     if (tc < tr.closest) {
       tr.closest = tc;
       tr.best = ref;
     }
-#else
-    if (ty == kSphere) {
-      if (hit_sphere_t<kX>(sc.spheres[ix], o, d, tr.tmin, tr.closest, t) && (kX || t < tr.closest)) {
-        tr.closest = t;
-        tr.best = ref;
-      }
-    } else if (ty == kQuad) {
-      if (hit_quad_t<kX>(sc.quads + 4 * ix, o, d, tr.tmin, tr.closest, t) && (kX || t < tr.closest)) {
-        tr.closest = t;
-        tr.best = ref;
-      }
-    } else {
-      if (hit_tri_t<kX>(sc.tris + 3 * ix, o, d, tr.tmin, tr.closest, t) && (kX || t < tr.closest)) {
-        tr.closest = t;
-        tr.best = ref;
-      }
-    }
-#endif
-#else
-    if (hit_leaf(sc, ref, o, d, tr.tmin, tr.closest, t) && t < tr.closest) {
-      tr.closest = t;
-      tr.best = ref;
-    }
-#endif
     return;
   }
 #if PTMI_PROBE == 2

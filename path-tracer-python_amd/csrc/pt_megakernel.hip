@@ -64,10 +64,6 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 #define PTMI_MK_SHADE_AT 24
 #endif
 
-#ifndef PTMI_MK_HDR_REUSE
-#define PTMI_MK_HDR_REUSE 1  // A/B: +0.8 % alone, with PTMI_STEP_FLAT +0.2 % more (profiles/r05/ab/ab_step_flat.log)
-#endif
-
 #ifndef PTMI_MK_STEP_UNROLL
 #define PTMI_MK_STEP_UNROLL 4  // A/B: 3 pops per header pass +1.9 % C2, +2.6 % C4 over 1 (round 1; 2: +1.5 %, 4: +1.6 %); round 4, with the 4-load node visits: 4 over 3 C2 +0.8 %, C5 +0.5 %, C4 +0.2 % (profiles/r04/ab/ab_r04su_step_unroll.log)
 #endif
@@ -418,12 +414,9 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       // and shading test sit on every wave's serial chain)
 #pragma unroll
       for (int u = 0; u < PTMI_MK_STEP_UNROLL; ++u)
-#if PTMI_MK_HDR_REUSE
-        // the first pop's busy lanes are the header's mask (no second compare)
+        // the first pop's busy lanes are the header's mask, not a second
+        // compare (A/B: +0.8 %, profiles/r05/ab/ab_step_flat.log)
         if (u == 0 ? __builtin_amdgcn_inverse_ballot_w64(mbusy) : tr.busy())
-#else
-        if (tr.busy())
-#endif
           trav_step<STACK, kMkBlock, PTMI_MK_DEFER>(sc, nodes, tr, st, ps.o, ps.dir);
 #if PTMI_PROBE == 2
       ++pr_steps;
