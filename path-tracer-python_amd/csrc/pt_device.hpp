@@ -497,6 +497,9 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 #ifndef PTMI_PROBE
 #define PTMI_PROBE 0
 #endif
+#ifndef PTMI_NODE_FIRST
+#define PTMI_NODE_FIRST 0
+#endif
 #if PTMI_PROBE
 __device__ unsigned long long g_probe[16];
 #endif
@@ -609,23 +612,9 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
   // fewer +1.0 / +1.4 / +1.0 % (ab_step_flat.log); independent type branches
   // with a candidate t +0.45 / +0.45 / +0.5 %, C3 +0.5 % (ab_leaf_tc.log).
   const unsigned long long m_leaf = pt_ballot(ref < 0), m_live = pt_ballot(__uint_as_float(ent.y) <= tr.closest);
-  unsigned long long m_def = 0ull;  // deferred lanes
-  if constexpr (DEFER > 0) {
-    const unsigned long long md = m_leaf & m_live;
-    const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
-    m_def = (md != 0ull && md != pt_ballot(true) && nd < (uint32_t)DEFER) ? md : 0ull;
-    if (m_def != 0ull) tr.sp += __builtin_amdgcn_inverse_ballot_w64(m_def) ? kSlot : 0u;  // kept on top
-  }
-  const unsigned long long m_go = m_live & ~m_def;  // lanes that test their popped entry in this step
-#if PTMI_PROBE == 1
-  if (!__builtin_amdgcn_inverse_ballot_w64(m_def)) {
-    atomicAdd(&g_probe[4], 1ull);                                                        // pops
-    if (!__builtin_amdgcn_inverse_ballot_w64(m_live)) atomicAdd(&g_probe[5], 1ull);      // culled pops
-    else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
-  }
-#endif
-  if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
-  if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {  // leaf: kernels.py:671-697
+  // leaf test (kernels.py:671-697) and node expansion (kernels.py:698-740),
+  // for the lanes of each kind
+  auto leaf_step = [&]() {
 #if PTMI_PROBE == 2
     tr.probe |= leaf_type(ref) == kSphere ? 1 : 2;
 #endif
@@ -646,13 +635,13 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
       tr.closest = tc;
       tr.best = ref;
     }
-    return;
-  }
+  };
+  auto node_step = [&]() {
 #if PTMI_PROBE == 2
-  tr.probe |= 4;
+    tr.probe |= 4;
 #endif
 #if PTMI_PROBE == 1
-  {  // debug probe: node visits and wave-uniform node visits (lane counts)
+    {  // debug probe: node visits and wave-uniform node visits (lane counts)
     const int32_t ru = __builtin_amdgcn_readfirstlane(ref);
     const bool uni = __ballot(ref != ru) == 0ull;
     atomicAdd(&g_probe[0], 1ull);
@@ -662,53 +651,84 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
       atomicAdd(&g_probe[2], 1ull);  // wave-level node steps
       atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
     }
+    }
+#endif
+    // internal: kernels.py:698-740, both children at once
+    const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
+    const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
+    const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
+    const float tmin = tr.tmin;
+    gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // the node at byte offset ref
+    const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
+    const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
+    const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
+    const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
+    const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
+    const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
+    const float E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
+    const float X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
+    const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
+    const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
+    // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
+    // x / y centres from the boxes just loaded, (min + max) * 0.5 as the
+    // reference computes them (bit-identical); the z centres come with the
+    // refs. A/B on MI355X (round 4, parity-identical), against loading all
+    // three (a fifth 16-B load per node): C3 +2.4 %, C2 +0.9 %, C5 +0.9 %, C4
+    // +-0 (profiles/r04/ab/ab_r04x_node_centres.log; the megakernel's
+    // texture-address unit is 70 % busy, profiles/r04/pmc_ta/); the refs alone
+    // as an 8-B load with the z centres computed too: C2 -4 %, C3 -2 %
+    // (ab_r04y_node_refs_only.log).
+    const pt_f2 cx = (lox + hix) * pt_f2s(0.5f), cy = (loy + hiy) * pt_f2s(0.5f), cz = {R.z, R.w};
+    const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
+    const bool ln = dist.x < dist.y;  // child 0 is the near one; the far child is pushed first
+    const bool h0 = X0 >= E0, h1 = X1 >= E1;
+    // Far first, then near, each kept only if its box is hit: the far child
+    // lands at sp and the near one at sp + slot when the far one is hit, else
+    // the near one at sp and the (dropped) far one at sp + slot, above the
+    // top. Child 0 takes the upper slot when (near and the far child 1 is hit)
+    // or (far and missed). Writing each child's {ref, E} straight to its slot
+    // needs no value selects. No bound check: an internal node at depth d has
+    // at most d pending entries, so sp + 2 slots <= max_leaf_depth + 1 <= STACK
+    // (enforced at dispatch) and the reference's overflow drop never triggers.
+    // up0 = ln ? h1 : !h0, as and/or of the compares' lane masks (SALU; a bool
+    // select would be materialised with four v_cndmask)
+    const unsigned long long mln = pt_ballot(ln), mh0 = pt_ballot(h0), mh1 = pt_ballot(h1);
+    const bool up0 = __builtin_amdgcn_inverse_ballot_w64((mln & mh1) | (~mln & ~mh0));
+    const uint32_t lo = tr.sp, hi = tr.sp + kSlot;
+    stack_store<STACK, LDS, SB>(st, lim, up0 ? hi : lo, __float_as_uint(R.x), __float_as_uint(E0));
+    stack_store<STACK, LDS, SB>(st, lim, up0 ? lo : hi, __float_as_uint(R.y), __float_as_uint(E1));
+    tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
+  };
+#if PTMI_NODE_FIRST
+  // the node lanes first: their loads go out before the deferral's scalar
+  // chain (the deferral only concerns leaf lanes)
+  if (__builtin_amdgcn_inverse_ballot_w64(m_live & ~m_leaf)) node_step();
+#endif
+  unsigned long long m_def = 0ull;  // deferred lanes
+  if constexpr (DEFER > 0) {
+    const unsigned long long md = m_leaf & m_live;
+    const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
+    m_def = (md != 0ull && md != pt_ballot(true) && nd < (uint32_t)DEFER) ? md : 0ull;
+    if (m_def != 0ull) tr.sp += __builtin_amdgcn_inverse_ballot_w64(m_def) ? kSlot : 0u;  // kept on top
+  }
+  const unsigned long long m_go = m_live & ~m_def;  // lanes that test their popped entry in this step
+#if PTMI_PROBE == 1
+  if (!__builtin_amdgcn_inverse_ballot_w64(m_def)) {
+    atomicAdd(&g_probe[4], 1ull);                                                        // pops
+    if (!__builtin_amdgcn_inverse_ballot_w64(m_live)) atomicAdd(&g_probe[5], 1ull);      // culled pops
+    else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
   }
 #endif
-  // internal: kernels.py:698-740, both children at once
-  const pt_f2 ox = pt_f2s(o.x), oy = pt_f2s(o.y), oz = pt_f2s(o.z);
-  const pt_f2 ix = pt_f2s(tr.inv.x), iy = pt_f2s(tr.inv.y), iz = pt_f2s(tr.inv.z);
-  const pt_f2 dx = pt_f2s(d.x), dy = pt_f2s(d.y), dz = pt_f2s(d.z);
-  const float tmin = tr.tmin;
-  gf4* nd = (gf4*)((const __attribute__((address_space(1))) char*)nodes + (uint32_t)ref);  // the node at byte offset ref
-  const pt_f4 A = nd[0], B = nd[1], C = nd[2], R = nd[3];
-  const pt_f2 lox = {A.x, A.y}, loy = {A.z, A.w}, loz = {B.x, B.y};
-  const pt_f2 hix = {B.z, B.w}, hiy = {C.x, C.y}, hiz = {C.z, C.w};
-  const pt_f2 t0x = (lox - ox) * ix, t1x = (hix - ox) * ix;
-  const pt_f2 t0y = (loy - oy) * iy, t1y = (hiy - oy) * iy;
-  const pt_f2 t0z = (loz - oz) * iz, t1z = (hiz - oz) * iz;
-  const float E0 = pt_maxf(pt_maxf(pt_minf(t0x.x, t1x.x), pt_minf(t0y.x, t1y.x)), pt_maxf(pt_minf(t0z.x, t1z.x), tmin));
-  const float X0 = pt_minf(pt_minf(pt_maxf(t0x.x, t1x.x), pt_maxf(t0y.x, t1y.x)), pt_maxf(t0z.x, t1z.x));
-  const float E1 = pt_maxf(pt_maxf(pt_minf(t0x.y, t1x.y), pt_minf(t0y.y, t1y.y)), pt_maxf(pt_minf(t0z.y, t1z.y), tmin));
-  const float X1 = pt_minf(pt_minf(pt_maxf(t0x.y, t1x.y), pt_maxf(t0y.y, t1y.y)), pt_maxf(t0z.y, t1z.y));
-  // projected centre distances dot(centre - o, d), (x + y) + z order (kernels.py:707-713)
-  // x / y centres from the boxes just loaded, (min + max) * 0.5 as the
-  // reference computes them (bit-identical); the z centres come with the
-  // refs. A/B on MI355X (round 4, parity-identical), against loading all
-  // three (a fifth 16-B load per node): C3 +2.4 %, C2 +0.9 %, C5 +0.9 %, C4
-  // +-0 (profiles/r04/ab/ab_r04x_node_centres.log; the megakernel's
-  // texture-address unit is 70 % busy, profiles/r04/pmc_ta/); the refs alone
-  // as an 8-B load with the z centres computed too: C2 -4 %, C3 -2 %
-  // (ab_r04y_node_refs_only.log).
-  const pt_f2 cx = (lox + hix) * pt_f2s(0.5f), cy = (loy + hiy) * pt_f2s(0.5f), cz = {R.z, R.w};
-  const pt_f2 dist = ((cx - ox) * dx + (cy - oy) * dy) + (cz - oz) * dz;
-  const bool ln = dist.x < dist.y;  // child 0 is the near one; the far child is pushed first
-  const bool h0 = X0 >= E0, h1 = X1 >= E1;
-  // Far first, then near, each kept only if its box is hit: the far child
-  // lands at sp and the near one at sp + slot when the far one is hit, else
-  // the near one at sp and the (dropped) far one at sp + slot, above the
-  // top. Child 0 takes the upper slot when (near and the far child 1 is hit)
-  // or (far and missed). Writing each child's {ref, E} straight to its slot
-  // needs no value selects. No bound check: an internal node at depth d has
-  // at most d pending entries, so sp + 2 slots <= max_leaf_depth + 1 <= STACK
-  // (enforced at dispatch) and the reference's overflow drop never triggers.
-  // up0 = ln ? h1 : !h0, as and/or of the compares' lane masks (SALU; a bool
-  // select would be materialised with four v_cndmask)
-  const unsigned long long mln = pt_ballot(ln), mh0 = pt_ballot(h0), mh1 = pt_ballot(h1);
-  const bool up0 = __builtin_amdgcn_inverse_ballot_w64((mln & mh1) | (~mln & ~mh0));
-  const uint32_t lo = tr.sp, hi = tr.sp + kSlot;
-  stack_store<STACK, LDS, SB>(st, lim, up0 ? hi : lo, __float_as_uint(R.x), __float_as_uint(E0));
-  stack_store<STACK, LDS, SB>(st, lim, up0 ? lo : hi, __float_as_uint(R.y), __float_as_uint(E1));
-  tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
+#if PTMI_NODE_FIRST
+  if (__builtin_amdgcn_inverse_ballot_w64(m_go & m_leaf)) leaf_step();
+#else
+  if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
+  if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {
+    leaf_step();
+    return;
+  }
+  node_step();
+#endif
 }
 
 // ---------------------------------------------------------------- stackless traversal
