@@ -497,9 +497,6 @@ __device__ __forceinline__ pt_f2 pt_f2s(float v) { return pt_f2{v, v}; }
 #ifndef PTMI_PROBE
 #define PTMI_PROBE 0
 #endif
-#ifndef PTMI_NODE_FIRST
-#define PTMI_NODE_FIRST 0
-#endif
 #if PTMI_PROBE
 __device__ unsigned long long g_probe[16];
 #endif
@@ -699,16 +696,21 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     stack_store<STACK, LDS, SB>(st, lim, up0 ? lo : hi, __float_as_uint(R.y), __float_as_uint(E1));
     tr.sp += (h0 ? kSlot : 0u) + (h1 ? kSlot : 0u);
   };
-#if PTMI_NODE_FIRST
-  // the node lanes first: their loads go out before the deferral's scalar
-  // chain (the deferral only concerns leaf lanes)
-  if (__builtin_amdgcn_inverse_ballot_w64(m_live & ~m_leaf)) node_step();
-#endif
+  // With deferral the node lanes go first: their loads go out before the
+  // deferral's scalar chain, which concerns leaf lanes only. A/B on MI355X
+  // (parity-identical), with the chain itself shortened (1 <= nd < DEFER as
+  // one unsigned compare, no early-out branch): C2 +1.3 %, C4 +1.2 %, C5
+  // +1.2 % (node lanes first alone +0.7 / +0.7 / +0.7 %, the chain alone
+  // +0.5 / +0.3 / +0.2 %); node lanes first in the wavefront's traversals
+  // (no deferral): C3 -1.1 %, mesh fog +0.6 % (profiles/r05/ab/ab_node_first.log).
+  if constexpr (DEFER > 0) {
+    if (__builtin_amdgcn_inverse_ballot_w64(m_live & ~m_leaf)) node_step();
+  }
   unsigned long long m_def = 0ull;  // deferred lanes
   if constexpr (DEFER > 0) {
     const unsigned long long md = m_leaf & m_live;
     const uint32_t nd = __builtin_popcount((uint32_t)md) + __builtin_popcount((uint32_t)(md >> 32));
-    m_def = (md != 0ull && md != pt_ballot(true) && nd < (uint32_t)DEFER) ? md : 0ull;
+    m_def = (nd - 1u < (uint32_t)(DEFER - 1) && md != pt_ballot(true)) ? md : 0ull;  // 1 <= nd < DEFER
     if (m_def != 0ull) tr.sp += __builtin_amdgcn_inverse_ballot_w64(m_def) ? kSlot : 0u;  // kept on top
   }
   const unsigned long long m_go = m_live & ~m_def;  // lanes that test their popped entry in this step
@@ -719,16 +721,16 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
     else if (ref < 0) atomicAdd(&g_probe[6 + (leaf_type(ref) == kSphere ? 0 : 1)], 1ull);  // leaf tests
   }
 #endif
-#if PTMI_NODE_FIRST
-  if (__builtin_amdgcn_inverse_ballot_w64(m_go & m_leaf)) leaf_step();
-#else
-  if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
-  if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {
-    leaf_step();
-    return;
+  if constexpr (DEFER > 0) {
+    if (__builtin_amdgcn_inverse_ballot_w64(m_go & m_leaf)) leaf_step();
+  } else {
+    if (!__builtin_amdgcn_inverse_ballot_w64(m_go)) return;
+    if (__builtin_amdgcn_inverse_ballot_w64(m_leaf)) {
+      leaf_step();
+      return;
+    }
+    node_step();
   }
-  node_step();
-#endif
 }
 
 // ---------------------------------------------------------------- stackless traversal
