@@ -102,7 +102,7 @@ constexpr int kWfBlock = PTMI_WF_BLOCK;
 // waves measured -1.5 % on round 3's in-place slots (profiles/r03/ab/ab_wf_spill.log)
 // and +0.8 % on round 5's compacted buffers (PTMI_WF_SPILL_MIN_STACK below). A
 // 16-slot wf_intersect padded down to 4 waves/SIMD loses 8 % (3 waves: 18 %).
-#define PTMI_WF_ISECT_LDS 11
+#define PTMI_WF_ISECT_LDS 10
 #endif
 #ifndef PTMI_WF_SPILL_MAX_STACK
 #define PTMI_WF_SPILL_MAX_STACK 20  // kernels of 17 to this many stack slots spill; deeper ones keep them all in LDS
@@ -123,6 +123,19 @@ constexpr int isect_lds() {
           PTMI_WF_ISECT_LDS < STACK)
              ? PTMI_WF_ISECT_LDS
              : STACK;
+}
+// ... and with 10 LDS slots (10 KiB per 2-wave block: 8 waves/SIMD) the
+// kernel is held to the 8-wave VGPR budget (64 VGPRs; 100 B/lane of scratch
+// instead of 52): A/B on MI355X, parity-identical, against 11 slots at 7 waves
+// (70 VGPRs): C3 +1.5 % (bench.py 2033 vs 2003), mesh fog +0.7 %
+// (profiles/r05/ab/ab_wf_isect_8waves.log). Kernels that keep more slots in
+// LDS (and the stackless walk) get no bound.
+#ifndef PTMI_WF_ISECT_MIN_WAVES
+#define PTMI_WF_ISECT_MIN_WAVES 8
+#endif
+template <int STACK, int TRAV>
+constexpr int isect_min_waves() {
+  return (isect_lds<STACK, TRAV>() < STACK && isect_lds<STACK, TRAV>() <= 10) ? PTMI_WF_ISECT_MIN_WAVES : 1;
 }
 // Wave priority (s_setprio) of the stage kernels, which run side by side from
 // the 4 pipes: -1 = none (A/B switches).
@@ -748,7 +761,7 @@ __device__ __forceinline__ void wf_intersect_refill(const DevScene& sc, const De
 // lasts. Writes the hit record (8 B) and one list entry (4 B) per ray; a path
 // end reads thr (16 B) and writes its staging slot.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-__global__ __launch_bounds__(kWfBlock) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
+__global__ __launch_bounds__(kWfBlock, (isect_min_waves<STACK, TRAV>())) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
   constexpr int LDS = isect_lds<STACK, TRAV>();
   __shared__ uint2 lds_stack[LDS * kWfBlock];
