@@ -30,6 +30,7 @@
 #                         for the default build and every variants/*.so (MK_VARIANTS: only those), two rounds
 # Every step has its own time limit; the script stops at the first failure.
 set -u
+shopt -s nullglob  # no variants built: the variant loops run over none
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"
