@@ -639,15 +639,15 @@ __device__ __forceinline__ void trav_step(const DevScene& sc, const float4* node
 #endif
 #if PTMI_PROBE == 1
     {  // debug probe: node visits and wave-uniform node visits (lane counts)
-    const int32_t ru = __builtin_amdgcn_readfirstlane(ref);
-    const bool uni = __ballot(ref != ru) == 0ull;
-    atomicAdd(&g_probe[0], 1ull);
-    if (uni) atomicAdd(&g_probe[1], 1ull);
-    const unsigned long long act = __ballot(true);
-    if (__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) == 0) {
-      atomicAdd(&g_probe[2], 1ull);  // wave-level node steps
-      atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
-    }
+      const int32_t ru = __builtin_amdgcn_readfirstlane(ref);
+      const bool uni = __ballot(ref != ru) == 0ull;
+      atomicAdd(&g_probe[0], 1ull);
+      if (uni) atomicAdd(&g_probe[1], 1ull);
+      const unsigned long long act = __ballot(true);
+      if (__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u)) == 0) {
+        atomicAdd(&g_probe[2], 1ull);  // wave-level node steps
+        atomicAdd(&g_probe[3], (unsigned long long)__popcll(act));  // active lanes in them
+      }
     }
 #endif
     // internal: kernels.py:698-740, both children at once
