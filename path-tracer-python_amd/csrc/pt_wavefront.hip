@@ -1208,7 +1208,11 @@ hipError_t pipe_streams_init(PipeStreams* ps) {
 #define PTMI_WF_DRAIN_AT 16
 #endif
 #ifndef PTMI_WF_CAPACITY_LOG2
-#define PTMI_WF_CAPACITY_LOG2 21  // rays per iteration (all pipes); A/B: 2^21 +3 % over 2^20 (C3, mesh fog)
+// rays per iteration (all pipes). A/B: 2^21 +3 % over 2^20 (C3, mesh fog);
+// with the 8-wave wf_intersect (late round 5) 2^22 over 2^21: mesh fog +5 %
+// (two runs), C3 +1.6 % / +-0 (C3 varies +-1.5 %); 2^23: mesh fog +9 %, C3
+// -2 % (profiles/r05/ab/ab_wf_capacity_8waves.log)
+#define PTMI_WF_CAPACITY_LOG2 22
 #endif
 constexpr int32_t kMaxCapacity = 1 << PTMI_WF_CAPACITY_LOG2;
 std::atomic<int32_t> g_drain_at{PTMI_WF_DRAIN_AT};
@@ -1228,7 +1232,7 @@ Layout layout(int32_t npix, int32_t batch) {
   int64_t items = (int64_t)npix * batch;
   // rays per iteration: 2^21 (or the batch's items if fewer), whatever the
   // frame size — the pool refills the buffers, so a 4K frame needs no more
-  // (the ray buffers are 56 B x 12 positions per ray: 1.4 GB at 2^21)
+  // (the ray buffers are 56 B x 12 positions per ray: 2.8 GB at 2^22)
   int64_t cap = kMaxCapacity;
   if (items < cap) cap = items;
   cap = (cap + kPipes * kSlotQuantum - 1) / (kPipes * kSlotQuantum) * (kPipes * kSlotQuantum);

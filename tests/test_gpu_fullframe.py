@@ -20,7 +20,7 @@ CASES = [
     ('vol2_final_scene', 800, 'wf', 4),
     ('cornell_mesh_fog', 1024, 'mk', 2),
     ('vol2_final_scene_comparison', 3840, 'mk', 1),
-    # the 4K frame (8.3 M pixels) through the wavefront's 2^21 rays per iteration
+    # the 4K frame (8.3 M pixels) through the wavefront's 2^22 rays per iteration
     ('vol2_final_scene_comparison', 3840, 'wf', 1),
 ]
 

@@ -324,8 +324,8 @@ def test_wavefront_tail_traces_the_items_groups_still_hold(drain_at):
     """the tail launch starts once a pipe's live slots fall
     below capacity / drain_at, which only says the shards are empty — a
     64-slot group may still hold items it fetched and has not handed out
-    (wb.grp). wf_drain must trace those too. The whole 800x800 frame x 4 spp
-    is 2.56 M items for 2^21 queue slots, so the tail begins while groups
+    (wb.grp). wf_drain must trace those too. The whole 800x800 frame x 8 spp
+    is 5.12 M items for 2^22 rays per iteration, so the tail begins while groups
     hold items; drain_at = 1 starts it as soon as the pool is dry (most
     groups then hold some), 2 half-way, 0 never (one intersect + scatter
     launch per wave to the end). Every path is traced exactly once: the
@@ -335,7 +335,7 @@ def test_wavefront_tail_traces_the_items_groups_still_hold(drain_at):
     from parity_helpers import compare, oracle_render
     from ptmi import device, _lib
     sa, cam, bg = scene_inputs('vol2_final_scene', 800)
-    W, H, spp = cam['width'], cam['height'], 4
+    W, H, spp = cam['width'], cam['height'], 8  # more items than the 2^22 rays per iteration
     lib = _lib.load()
     integ = device.Integrator(device.DeviceScene.from_arrays(sa))
     fr = device.make_frame(cam, bg, 50, 0, W, H)
