@@ -1230,7 +1230,7 @@ constexpr size_t kSpillPipeBytes = (size_t)kSpillSlots * (PTMI_WF_MAX_BLOCKS / k
 Layout layout(int32_t npix, int32_t batch) {
   Layout L;
   int64_t items = (int64_t)npix * batch;
-  // rays per iteration: 2^21 (or the batch's items if fewer), whatever the
+  // rays per iteration: 2^22 (or the batch's items if fewer), whatever the
   // frame size — the pool refills the buffers, so a 4K frame needs no more
   // (the ray buffers are 56 B x 12 positions per ray: 2.8 GB at 2^22)
   int64_t cap = kMaxCapacity;
