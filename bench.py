@@ -13,8 +13,9 @@ over the whole image for spp-per-step samples. Scene = the reference's own
 vol2_final_scene compiled arrays captured at random.seed(1234)
 (tests/golden/vol2_final_scene.npz), camera from the reference's camera math.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU. By default the image is tile-sharded (BASELINE.json
+Multi-GPU (python3 bench.py --gpus N, or python -m torch.distributed.run ...
+bench.py --gpus N): one process per GPU; without a launcher's RANK in the
+environment bench.py starts the N ranks itself (ptmi.launch). By default the image is tile-sharded (BASELINE.json
 configs[4]): rank r renders the interleaved row bands it owns for every sample
 of every step, so the total workload (W x H x spp_per_step x steps) is fixed
 and N GPUs split it (strong scaling); the bands' height is chosen so every
@@ -83,6 +84,17 @@ ALGO_BYTES = {
 }
 
 
+def kernel_units(kernel, segments, tail, samples, pixels, prof):
+    """Units of work ``kernel`` processed in the timed steps (the unit of
+    ALGO_BYTES[kernel]): the wavefront's segments traced by its tail launch
+    (device counter [5], `tail`) are wf_drain's, the rest wf_intersect's and
+    wf_scatter's; a resolve's unit is a pixel per launch."""
+    return {'wf_intersect': segments - tail, 'wf_scatter': segments - tail, 'megakernel': samples,
+            'wf_generate': 0, 'wf_drain': tail,
+            'wf_resolve': pixels * prof.get('wf_resolve', {}).get('launches', 0),
+            'mk_resolve': pixels * prof.get('mk_resolve', {}).get('launches', 0)}[kernel]
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
@@ -99,6 +111,10 @@ def parse(argv=None):
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--save-image', default='')
+    p.add_argument('--save-accum', default='',
+                   help='rank 0 writes the assembled float32 accumulator (H, W, 3) to this .npy file')
+    p.add_argument('--launch-timeout', type=float, default=3600.0,
+                   help='--gpus N > 1 without a launcher: seconds the ranks may run before they are stopped')
     p.add_argument('--dist-backend', choices=('nccl', 'gloo'), default=None,
                    help='nccl = RCCL over xGMI (the product path, the default for --gpus > 1); gloo only to '
                         'rehearse the multi-rank flow with several ranks on one GPU (host-side collective). '
@@ -310,6 +326,13 @@ def _free_port():
 
 def main():
     a = parse()
+    if a.gpus > 1 and 'RANK' not in os.environ:
+        # `python3 bench.py --gpus N` with no launcher: start the N ranks here
+        # (ptmi.launch), before anything in this process touches the GPU, and
+        # exit with the first failing rank's code; rank 0 prints the line
+        from ptmi.launch import launch_ranks
+        sys.exit(launch_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], a.gpus,
+                              timeout_s=a.launch_timeout))
     import torch
     import torch.distributed as dist
     from ptmi import _lib
@@ -407,10 +430,7 @@ def main():
     # segments traced by the wavefront's tail launch (wf_drain) belong to its
     # time, not to wf_intersect's / wf_scatter's
     tail = (integ.tail_segments() or 0) if a.variant == 'wf' else 0
-    units = {'wf_intersect': cnt['segments'] - tail, 'wf_scatter': cnt['segments'] - tail,
-             'megakernel': samples_rank,
-             'wf_generate': 0, 'wf_drain': tail, 'wf_resolve': W * rows_rank * prof['wf_resolve']['launches'],
-             'mk_resolve': W * rows_rank * prof['mk_resolve']['launches']}[dom]
+    units = kernel_units(dom, cnt['segments'], tail, samples_rank, W * rows_rank, prof)
     dom_ms = prof[dom]['busy_ms']
     launches = prof[dom]['launches']
     avg_launch_ms = dom_ms / max(1, launches)
@@ -480,6 +500,9 @@ def main():
     elif rank == 0:
         out['cpu_baseline'] = None
     if rank == 0:
+        if a.save_accum:
+            import numpy as np
+            np.save(a.save_accum, acc.cpu().numpy())
         if a.save_image:
             from PIL import Image
             # tiles: every pixel has sps * steps samples; samples: each rank added its own

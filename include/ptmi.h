@@ -232,10 +232,10 @@ size_t ptmi_wf_workspace_bytes(const ptmi_frame *frame, int32_t batch_samples);
 int ptmi_wf_render(const ptmi_scene_view *scene, const ptmi_frame *frame, void *workspace,
                    size_t workspace_bytes, float *accum, int32_t sample_begin, int32_t sample_count,
                    uint64_t *counters, void *stream);
-/* Schedule knob of ptmi_wf_render's tail (no effect on results): once a
- * pipe's live slots fall below capacity / divisor (the work pool is then
- * empty), one launch finishes its remaining paths and the items its slot
- * groups still hold, instead of one intersect and one scatter launch per
+/* Schedule knob of ptmi_wf_render's tail (no effect on results): once the
+ * work pool is dry and a pipe traces fewer than capacity / divisor rays per
+ * iteration, one launch finishes the paths still in its ray buffer (its
+ * continuing rays), instead of one intersect and one scatter launch per
  * remaining wave. 0 = no tail launch; default 16. Process-wide, read at the
  * start of each batch. Returns the previous divisor, or PTMI_EINVAL for a
  * negative one. ABI v7. */

@@ -263,11 +263,12 @@ class MI355XRenderer:
         * 'survived', 'avg_depth_killed', 'avg_depth_survived': 0 / 0.0, as in
           the reference: the device does not count paths that passed the RR
           test, nor depth sums. Their names are listed under 'uncounted'.
-        * 'total_rr_paths' = killed + survived and 'kill_rate' = killed /
-          total_rr_paths x 100 (0.0 when empty): the reference's formulas
-          (renderer.py:488-489), so with survived uncounted 'kill_rate' is 100
-          whenever anything was killed. 'kill_rate_of_paths' = killed / all
-          paths x 100 is the informative rate.
+        * 'total_rr_paths' = killed + survived, as in the reference
+          (renderer.py:488). 'kill_rate' is killed / paths x 100, the share of
+          all traced paths that Russian roulette ended (0.0 when none were
+          traced): the reference's killed / total_rr_paths would read 100 %
+          whenever anything was killed, because survived is uncounted here, so
+          that formula is not published.
         * Extra keys: 'paths', 'depth_cap' (paths ended by the depth / wave
           budget), 'uncounted'."""
         c = self.integrator.read_counters() or {}
@@ -275,9 +276,8 @@ class MI355XRenderer:
         total = killed + survived
         paths = int(c.get('paths', 0))
         return {'killed': killed, 'survived': survived, 'total_rr_paths': total,
-                'kill_rate': (killed / total * 100) if total > 0 else 0.0,
+                'kill_rate': 100.0 * killed / paths if paths else 0.0,
                 'avg_depth_killed': 0.0, 'avg_depth_survived': 0.0,
-                'kill_rate_of_paths': 100.0 * killed / paths if paths else 0.0,
                 'paths': paths, 'depth_cap': int(c.get('depth_cap', 0)),
                 'uncounted': ('survived', 'avg_depth_killed', 'avg_depth_survived')}
 

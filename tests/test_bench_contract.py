@@ -117,7 +117,16 @@ def test_every_preset_has_a_valu_row_from_the_same_collection(preset, kernel):
 
 def test_wavefront_tail_segments_are_the_drains_units():
     """Segments the wavefront traced in its tail launch (counter [5]) are
-    wf_drain's units, not wf_intersect's."""
-    import inspect
-    src = inspect.getsource(bench.main)
-    assert "'wf_intersect': cnt['segments'] - tail" in src and "'wf_drain': tail" in src
+    wf_drain's units, not wf_intersect's or wf_scatter's (ADVICE r04/r05:
+    checked on the mapping itself with made-up counters)."""
+    prof = {'wf_resolve': {'launches': 3}, 'mk_resolve': {'launches': 2}}
+    seg, tail, samples, pix = 1_000_000, 12_345, 640_000, 640_000
+    assert bench.kernel_units('wf_intersect', seg, tail, samples, pix, prof) == seg - tail
+    assert bench.kernel_units('wf_scatter', seg, tail, samples, pix, prof) == seg - tail
+    assert bench.kernel_units('wf_drain', seg, tail, samples, pix, prof) == tail
+    assert bench.kernel_units('megakernel', seg, 0, samples, pix, prof) == samples
+    assert bench.kernel_units('wf_resolve', seg, tail, samples, pix, prof) == 3 * pix
+    assert bench.kernel_units('mk_resolve', seg, 0, samples, pix, prof) == 2 * pix
+    # every kernel the roofline can name has a unit
+    for k in bench.ALGO_BYTES:
+        bench.kernel_units(k, seg, tail, samples, pix, prof)

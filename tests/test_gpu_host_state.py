@@ -321,13 +321,13 @@ _FULL_FRAME_ORACLE = {}
 
 @pytest.mark.parametrize('drain_at', [1, 2, 0])
 def test_wavefront_tail_traces_the_items_groups_still_hold(drain_at):
-    """the tail launch starts once a pipe's live slots fall
-    below capacity / drain_at, which only says the shards are empty — a
-    64-slot group may still hold items it fetched and has not handed out
-    (wb.grp). wf_drain must trace those too. The whole 800x800 frame x 8 spp
-    is 5.12 M items for 2^22 rays per iteration, so the tail begins while groups
-    hold items; drain_at = 1 starts it as soon as the pool is dry (most
-    groups then hold some), 2 half-way, 0 never (one intersect + scatter
+    """the tail launch starts once the work pool is dry
+    and a pipe traces fewer than capacity / drain_at rays per iteration;
+    wf_drain must then finish every path still in the pipe's ray buffer and
+    lose none (no fresh item is due: the pool is dry). The whole 800x800
+    frame x 8 spp is 5.12 M items for 2^22 rays per iteration, so the tail
+    begins while the buffers are still well filled; drain_at = 1 starts it as
+    soon as the pool is dry, 2 half-way, 0 never (one intersect + scatter
     launch per wave to the end). Every path is traced exactly once: the
     paths counter is W x H x spp, the image and the counters equal the
     oracle's bit for bit, and the tail traced segments whenever it ran."""
@@ -353,7 +353,7 @@ def test_wavefront_tail_traces_the_items_groups_still_hold(drain_at):
     drains = kt.result['wf_drain']['launches']
     assert gst['paths'] == W * H * spp
     if drain_at:
-        assert 1 <= drains <= 4 and tail > 0
+        assert 1 <= drains <= 4 and 0 < tail <= gst['segments']
     else:
         assert drains == 0 and tail == 0
     if 'ref' not in _FULL_FRAME_ORACLE:
