@@ -41,6 +41,17 @@ static inline FastDiv fast_div(uint32_t d) {
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (uint32_t)(((uint64_t)n * f.m) >> f.sh); }
 constexpr int kBlock = 256;
 
+// Register-budget stress build (libptmi_stress.so, tests/test_gpu_stress_build.py):
+// PTMI_STRESS_WAVES = N raises every render kernel's minimum waves per SIMD to
+// N, i.e. caps its VGPRs so that it spills. A legal register budget must not
+// change a result; the stress build renders the parity cases against the
+// oracle, so code that depends on what an inactive lane's register holds
+// (round 6, cont_position in pt_wavefront.hip) fails there. 0: off.
+#ifndef PTMI_STRESS_WAVES
+#define PTMI_STRESS_WAVES 0
+#endif
+constexpr int stress_waves(int w) { return PTMI_STRESS_WAVES > w ? PTMI_STRESS_WAVES : w; }
+
 enum : int32_t { kSphere = 0, kTriangle = 1, kQuad = 2 };
 
 struct DevScene {
@@ -129,18 +140,12 @@ __device__ __forceinline__ pt_v3 random_unit_vector(Rng& r) {  // kernels.py:29-
 // parity-identical) against the divergent site: C4 +1.4 %, C2 +0.2 %, C5
 // +0.1 % (the split of the shading code around the uniform site alone: C4
 // -1.3 %; profiles/r04/ab/ab_r04r_wave_ruv.log).
-#ifndef PTMI_RUV_WAVE_NOINLINE
-#define PTMI_RUV_WAVE_NOINLINE 0  // inlined: A/B within noise of the call (C4 +1.4 vs +1.3 %, C5 +0.1 vs -0.2 %)
-#endif
+// Inlined: A/B within noise of a call (C4 +1.4 vs +1.3 %, C5 +0.1 vs -0.2 %).
 struct RuvOut {
   pt_v3 v;
   uint32_t n;  // the lane's counter after its draws
 };
-#if PTMI_RUV_WAVE_NOINLINE
-__device__ __attribute__((noinline)) RuvOut random_unit_vector_wave(uint32_t key, uint32_t ctr, bool need, int lane) {
-#else
 __device__ __forceinline__ RuvOut random_unit_vector_wave(uint32_t key, uint32_t ctr, bool need, int lane) {
-#endif
   unsigned long long pend = __builtin_amdgcn_ballot_w64(need);
   const uint32_t k0 = (uint32_t)__popcll(pend);
   if (k0 > 32u) {  // too many for a group each: the plain loop
@@ -335,26 +340,17 @@ __device__ __forceinline__ bool hit_tri_v(const float4 a, const float4 b, const 
   return false;
 }
 
-#ifndef PTMI_TRI_E2Z_DWORD
-#define PTMI_TRI_E2Z_DWORD 0
-#endif
+// (A/B, round 5, not kept: a dword load of e2.z instead of the third 16 B,
+// C4 +0.2 %, noise.)
 template <bool EXCL = false>
 __device__ __forceinline__ bool hit_tri_t(const float4* __restrict__ tr, pt_v3 o, pt_v3 d, float tmin,
                                           float tmax, float& t) {
   typedef float pt_f4 __attribute__((ext_vector_type(4)));
   pt_f4 A = ((const pt_f4*)tr)[0], B = ((const pt_f4*)tr)[1];
-#if PTMI_TRI_E2Z_DWORD
-  // the test reads e2.z of the third 16 B only (the normal is read at shading)
-  float cx = ((const float*)tr)[8];
-  asm volatile("" : "+v"(A), "+v"(B), "+v"(cx));
-  return hit_tri_v<EXCL>(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w), make_float4(cx, 0.0f, 0.0f, 0.0f),
-                   o, d, tmin, tmax, t);
-#else
   pt_f4 C = ((const pt_f4*)tr)[2];
   asm volatile("" : "+v"(A), "+v"(B), "+v"(C));
   return hit_tri_v<EXCL>(make_float4(A.x, A.y, A.z, A.w), make_float4(B.x, B.y, B.z, B.w),
                          make_float4(C.x, C.y, C.z, C.w), o, d, tmin, tmax, t);
-#endif
 }
 
 __device__ __forceinline__ bool hit_leaf(const DevScene& sc, int32_t ref, pt_v3 o, pt_v3 d, float tmin,
@@ -506,11 +502,7 @@ __device__ unsigned long long g_probe[16];
 // last 16 B hold them precomputed and are not read. A/B on MI355X (round 4,
 // parity-identical): a 64-B stride without them, C2 -1.2 %, C4 -1.1 %, C5
 // -0.7 %, C3 +-0 (profiles/r04/ab/ab_r04z_node64.log), so the stride stays 80.
-#ifndef PTMI_NODE_BYTES
-#define PTMI_NODE_BYTES 80
-#endif
-static_assert(PTMI_NODE_BYTES == 80 || PTMI_NODE_BYTES == 64, "node stride: 80 or 64 B");
-constexpr uint32_t kNodeBytes = PTMI_NODE_BYTES;
+constexpr uint32_t kNodeBytes = 80;
 
 // In-flight traversal of one ray: begin (root test, push root) and one pop
 // of the loop per step, so a kernel can interleave steps of different rays'
@@ -1035,19 +1027,12 @@ __device__ __forceinline__ float perlin_turb3(const DevScene& sc, pt_v3 p) {  //
 // Perlin-textured hits otherwise runs the whole 3-octave evaluation (six
 // dependent table loads, ~400 VALU) for one or two lanes; here a pair costs
 // two table round trips and ~150 VALU. Call from wave-uniform control flow.
-#ifndef PTMI_WAVE_TURB_NOINLINE
 // A call, not inlined: A/B on MI355X (round 4, parity-identical) against the
 // inlined form, C2 +1.4 %, C5 +1.3 %, C4 +1.2 % — inlined, its temporaries
 // raise the register pressure of the whole persistent loop (scratch 36 ->
 // 112 B/lane); as a call, the kernel keeps its 96 VGPRs and no scratch
 // (profiles/r04/ab/ab_r04m_wave_turb.log).
-#define PTMI_WAVE_TURB_NOINLINE 1
-#endif
-#if PTMI_WAVE_TURB_NOINLINE
 __device__ __attribute__((noinline)) float perlin_turb3_wave(const DevScene& sc, bool need, pt_v3 p, int lane) {
-#else
-__device__ __forceinline__ float perlin_turb3_wave(const DevScene& sc, bool need, pt_v3 p, int lane) {
-#endif
   unsigned long long pend = pt_ballot(need);
   float res = 0.0f;
   const int c = lane & 31;

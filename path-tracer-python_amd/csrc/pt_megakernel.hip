@@ -95,15 +95,8 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // waves (profiles/r05/ab/ab_mk_handover.log). -1: PTMI_MK_PRIO_TRAV.
 #define PTMI_MK_PRIO_DRAIN 0
 #endif
-#ifndef PTMI_MK_PRIO_DRAIN_SHADE
-#define PTMI_MK_PRIO_DRAIN_SHADE -1  // shading priority of a draining wave (-1: PTMI_MK_PRIO_SHADE)
-#endif
-#ifndef PTMI_MK_PRIO_FULL
-#define PTMI_MK_PRIO_FULL -1  // traversal priority of a wave with >= PTMI_MK_PRIO_FULL_AT busy lanes (-1: off)
-#endif
-#ifndef PTMI_MK_PRIO_FULL_AT
-#define PTMI_MK_PRIO_FULL_AT 48
-#endif
+// (A/B, round 5, not kept: a draining wave's shading at its own priority,
+// and full waves' traversal above the others', profiles/r05/ab/.)
 // A/B, not kept (profiles/): Perlin-textured hits held until 4 or 8 of a wave
 // are ready, -1 to -1.5 % (r01/ab_mk_hold_noise.log); non-temporal staging
 // stores, +-0.3 % (r02/ab/ab_nontemporal.log); one random_unit_vector site per
@@ -132,29 +125,20 @@ __device__ __forceinline__ void start_path(const DevFrame& fr, int32_t px, int32
 // loop then runs once, to the wave's longest lane. A/B on MI355X (round 4,
 // parity-identical): C4 +2.1 %, C2 +-0.3 % (profiles/r04/ab/ab_r04i_split_knobs_ruv.log;
 // round 2 measured C2 -1.1 % with the code of the time).
-#ifndef PTMI_MK_WAVE_RUV
 // ... and that site in wave-uniform code, the wave sharing the loop
 // (random_unit_vector_wave, pt_device.hpp).
-#define PTMI_MK_WAVE_RUV 1
-#endif
-#ifndef PTMI_MK_WAVE_TURB
 // Turbulence of a shading round's Perlin-textured hits by the whole wave
 // (perlin_turb3_wave, pt_device.hpp). Ablation on MI355X (round 4, textures
 // replaced by constants, not parity): without the Perlin evaluation C2 +5 %,
 // C5 +4.8 %; without the image lookup +1.2 % (profiles/r04/ab/ab_r04l_texture_ablation.log).
-#define PTMI_MK_WAVE_TURB 1
-#endif
 #ifndef PTMI_MK_MIN_WAVES
 #define PTMI_MK_MIN_WAVES 4  // 4 waves/SIMD: <= 128 VGPRs, no spills (gfx950 hipcc 7.2)
 #endif
-#ifndef PTMI_MK_EXACT_STACK
 // Staged kernels for leaf depth 16-18 (17-19 slots, e.g. C4's torus BVH) get
 // exactly the slots they need instead of the 20-slot kernel, and the 5-wave
 // VGPR budget: 17 slots leave LDS for 18 one-wave blocks per CU instead of 16.
 // A/B on MI355X, C4 (leaf depth 16), parity-identical: 1357 -> 1414 Msamples/s
 // (+4.2 %; profiles/r02/ab/ab_exact_stack.log).
-#define PTMI_MK_EXACT_STACK 1
-#endif
 #ifndef PTMI_MK_MIN_WAVES_16
 // 16-slot kernels (leaf depth <= 15, e.g. vol2): 16 * 8 B * 64 lanes * 20
 // waves fill the 160 KiB LDS, and without SLP vectorization (Makefile) the
@@ -223,9 +207,6 @@ struct MkWork {
 };
 constexpr int kMkTile = 8;
 
-#ifndef PTMI_MK_BAND_TILES
-#define PTMI_MK_BAND_TILES 1
-#endif
 // Tile height (log2) of the staged megakernel's 64-pixel tiles. A frame's
 // local rows are its row bands packed together, so an 8x8 tile over 4-row
 // bands (bench.py --gpus 8 at 800 rows) would cover two runs of 4 image rows
@@ -233,7 +214,7 @@ constexpr int kMkTile = 8;
 // (16x4, 32x2, 64x1) stays inside one band. Which lane renders which pixel
 // changes nothing in the image (staging[sample][pixel], ordered resolve).
 static int mk_tile_rows_log2(const DevFrame& fr) {
-  if (!PTMI_MK_BAND_TILES || fr.band_stride <= 1) return 3;
+  if (fr.band_stride <= 1) return 3;
   const int32_t th = fr.band_rows & -fr.band_rows;
   return th >= 8 ? 3 : th >= 4 ? 2 : th >= 2 ? 1 : 0;
 }
@@ -250,7 +231,7 @@ template <int STACK, bool STAGED, int TRAV = PTMI_TRAV_STACK>
 // waves (96 at 5, 128 at 4).
 // TRAV = PTMI_TRAV_STACKLESS (STACK 1: no stack) walks the reference's
 // stackless traversal instead (TravSL, pt_device.hpp).
-__global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && STACK < 20) ? PTMI_MK_MIN_WAVES_16 : STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
+__global__ __launch_bounds__(kMkBlock, stress_waves(STACK < 20 ? PTMI_MK_MIN_WAVES_16 : STACK <= 20 ? PTMI_MK_MIN_WAVES : 1)) void mk_render_kernel(
     DevScene sc, DevFrame fr, float* __restrict__ accum, int32_t s_begin, int32_t s_count, int32_t chunk,
     float* __restrict__ staging, unsigned long long* __restrict__ counters, MkWork wk) {
   constexpr bool kPersist = STAGED;  // staged launches are persistent
@@ -399,14 +380,6 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
       const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
       if (nbusy == 0) break;
       if (nbusy <= (uint32_t)PTMI_MK_SHADE_AT && pt_ballot(trav && !tr.busy()) != 0ull) break;
-#if PTMI_MK_PRIO_FULL >= 0 && PTMI_MK_PRIO_TRAV >= 0
-      if (!(kPersist && drained && next >= wend)) {
-        if (nbusy >= (uint32_t)PTMI_MK_PRIO_FULL_AT)
-          __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_FULL);
-        else
-          __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_TRAV);
-      }
-#endif
 #if PTMI_PROBE == 2
       tr.probe = 0;
 #endif
@@ -435,25 +408,15 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     }
 #endif
 #if PTMI_MK_PRIO_TRAV >= 0
-#if PTMI_MK_PRIO_DRAIN >= 0 && PTMI_MK_PRIO_DRAIN_SHADE >= 0
-    if (kPersist && drained && next >= wend)
-      __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_DRAIN_SHADE);
-    else
-#endif
-      __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
+    __builtin_amdgcn_s_setprio(PTMI_MK_PRIO_SHADE);
 #endif
     PT_P4(0)  // traversal steps
     const bool shade_now = trav && !tr.busy();
-#if PTMI_MK_WAVE_TURB
     // Perlin-textured surface hits of this round: their turbulence by the
     // whole wave (perlin_turb3_wave), before the divergent shading below
     const bool pn = shade_now && ps.mode != kModeMediumExit && tr.any() && leaf_class(tr.best) == PTMI_CLASS_NOISE;
     float pturb = 0.0f;
     if (pt_ballot(pn) != 0ull) pturb = perlin_turb3_wave(sc, pn, pt_add(ps.o, pt_scale(ps.dir, tr.closest)), lane);
-#else
-    constexpr bool pn = false;
-    constexpr float pturb = 0.0f;
-#endif
     // Shading, in two halves around the round's one random_unit_vector site
     // (medium scatter, metal fuzz, isotropic), which runs in wave-uniform code
     // so that the wave can share its rejection loop (random_unit_vector_wave).
@@ -522,7 +485,6 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
     }
     PT_P4(2)  // material, medium step, surface scatter (first half)
     // one random_unit_vector site per round: medium, metal fuzz, isotropic
-#if PTMI_MK_WAVE_RUV
     if (pt_ballot(ruv != kRuvNone) != 0ull) {
       const RuvOut ro = random_unit_vector_wave(ps.rng.key, ps.rng.n, ruv != kRuvNone, lane);
       ps.rng.n = ro.n;
@@ -534,18 +496,6 @@ __global__ __launch_bounds__(kMkBlock, (STACK <= 16 || (PTMI_MK_EXACT_STACK && S
         scattered = scatter_end(sc, ruv, sref, mm, hp, n, ro.v, sdir, att);
       }
     }
-#else
-    if (ruv != kRuvNone) {
-      const pt_v3 v = random_unit_vector(ps.rng);
-      if (ruv == kRuvMedium) {
-        sdir = v;
-      } else {
-        Mat mm{};
-        mm.m0 = m0;
-        scattered = scatter_end(sc, ruv, sref, mm, hp, n, v, sdir, att);
-      }
-    }
-#endif
     PT_P4(3)  // unit vector (wave) and scatter_end
     if (shade_now) {
       if (!done && !to_medium) {
@@ -858,11 +808,9 @@ hipError_t mk_trace_staged(const DevScene& sc, const DevFrame& fr, int32_t stack
   if (fr.traversal == PTMI_TRAV_STACKLESS)
     return launch_mk_trace<1, PTMI_TRAV_STACKLESS>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= PTMI_MK_STAGED_MIN_STACK) return launch_mk_trace<16>(sc, fr, st, s_begin, nb, counters, stream);
-#if PTMI_MK_EXACT_STACK
   if (stack_needed == 17) return launch_mk_trace<17>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed == 18) return launch_mk_trace<18>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed == 19) return launch_mk_trace<19>(sc, fr, st, s_begin, nb, counters, stream);
-#endif
   if (stack_needed <= 20) return launch_mk_trace<20>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= 24) return launch_mk_trace<24>(sc, fr, st, s_begin, nb, counters, stream);
   if (stack_needed <= 32) return launch_mk_trace<32>(sc, fr, st, s_begin, nb, counters, stream);

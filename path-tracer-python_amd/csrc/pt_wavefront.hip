@@ -137,14 +137,6 @@ template <int STACK, int TRAV>
 constexpr int isect_min_waves() {
   return (isect_lds<STACK, TRAV>() < STACK && isect_lds<STACK, TRAV>() <= 10) ? PTMI_WF_ISECT_MIN_WAVES : 1;
 }
-// Wave priority (s_setprio) of the stage kernels, which run side by side from
-// the 4 pipes: -1 = none (A/B switches).
-#ifndef PTMI_WF_PRIO_ISECT
-#define PTMI_WF_PRIO_ISECT -1
-#endif
-#ifndef PTMI_WF_PRIO_SCATTER
-#define PTMI_WF_PRIO_SCATTER -1
-#endif
 #ifndef PTMI_WF_MAX_BLOCKS
 #define PTMI_WF_MAX_BLOCKS (2048 * 256 / PTMI_WF_BLOCK)  // all pipes together; A/B: 4096 -1.5 %, 8192 -3.5 % (C3)
 #endif
@@ -157,17 +149,12 @@ constexpr uint32_t kFresh = 0x80000000u;
 
 // Continuing-ray segments: kBins direction bins x kShards producer shards,
 // one counter each (kSegs <= 64: one wave holds them all, one per lane).
-// PTMI_WF_BINS 1 keeps the compaction without the sort. A/B on MI355X
-// (round 5, parity-identical; profiles/r05/ab/ab_wf_sort.log): against the
-// round-4 in-place slots (1685-1694 Msamples/s on C3, 705-708 on mesh fog)
-// the compacted buffers alone give 1889-1900 / 847-849, sorted by octant
-// 1914-1923 / 850-854; wf_intersect's lane efficiency 0.43 unsorted, 0.45
-// sorted (round 4: 0.32; profiles/r05/pmc/).
-#ifndef PTMI_WF_BINS
-#define PTMI_WF_BINS 8
-#endif
-constexpr int kBins = PTMI_WF_BINS;
-static_assert(kBins == 1 || kBins == 8, "direction bins: 1 (unsorted) or the 8 octants");
+// Sorting by octant, A/B on MI355X (round 5, parity-identical;
+// profiles/r05/ab/ab_wf_sort.log): against the round-4 in-place slots
+// (1685-1694 Msamples/s on C3, 705-708 on mesh fog) the compacted buffers
+// alone (one bin) give 1889-1900 / 847-849, sorted by octant 1914-1923 /
+// 850-854; wf_intersect's lane efficiency 0.43 unsorted, 0.45 sorted.
+constexpr int kBins = 8;
 constexpr int kSegs = kBins * kShards;
 #ifndef PTMI_WF_SEG_DIV
 #define PTMI_WF_SEG_DIV 16  // a segment's region holds capacity / this rays (4x an even share of 64 segments)
@@ -513,45 +500,55 @@ __device__ __forceinline__ SegTable seg_table(const WfBufs& wb, int32_t par) {
   T.bstart = sincl - span;
   const int32_t spans = __shfl(sincl, 63);
   const int32_t ov = __builtin_amdgcn_readfirstlane(min(s_load(ctl_ovf(wb, par)), wb.capacity));
-  T.ovf_start = spans;
+  // the wave-uniform fields in SGPRs (readfirstlane of converged values)
+  T.ovf_start = __builtin_amdgcn_readfirstlane(spans);
   T.ovf_n = ov;
-  T.fresh_start = spans + ((ov + 63) & ~63);
-  T.live = __shfl(incl, 63) + ov;
+  T.fresh_start = __builtin_amdgcn_readfirstlane(spans + ((ov + 63) & ~63));
+  T.live = __builtin_amdgcn_readfirstlane(__shfl(incl, 63) + ov);
   return T;
 }
 
 // Position of work index w0 + lane (w0 a wave's base, below fresh_start), or
-// -1 for a padding lane.
+// -1 for a padding lane. Call with every lane of the wave active: the bin's
+// start, size and shard offsets are read from other lanes' registers
+// (v_readlane), and a lane's register holds a defined value only while that
+// lane is active. All the reads therefore come before any lane-dependent
+// branch, and the padding test is a select. Round 6 root cause:
+// round 5's form left the padding lanes first (`if (j >= btot) return -1`)
+// and read the shard offsets of lanes b * 8 + k afterwards — in the last,
+// partly filled wave of a bin those are padding lanes, inactive at the read.
+// The shipped build kept the offsets in a register and read the right
+// values; a build held to 5 waves/SIMD spilled them and reloaded them from
+// scratch inside the branch, i.e. for the active lanes only, so some lanes
+// read another value's bits as an offset and traced a ray twice or not at all.
 __device__ __forceinline__ int32_t cont_position(const SegTable& T, const WfBufs& wb, int32_t w0) {
   const int lane = lane_id();
-  if (w0 >= T.ovf_start) {
+  if (w0 >= T.ovf_start) {  // wave-uniform
     const int32_t j = w0 - T.ovf_start + lane;
     return j < T.ovf_n ? ovf_base(wb) + j : -1;
   }
   const unsigned long long m = pt_ballot(lane < kBins && T.bstart <= w0 && w0 < T.bstart + T.btot);
   if (m == 0ull) return -1;  // (a wave base never falls in a bin's padding alone: bins are padded to < 64 more)
   const int32_t b = __ffsll((long long)m) - 1;  // wave-uniform: the bin this wave reads
-  const int32_t j = w0 - __builtin_amdgcn_readlane(T.bstart, b) + lane;
-  if (j >= __builtin_amdgcn_readlane(T.btot, b)) return -1;
+  const int32_t bstart = __builtin_amdgcn_readlane(T.bstart, b), btot = __builtin_amdgcn_readlane(T.btot, b);
+  int32_t pk[kShards];  // entries of the bin's lower shards, per shard (wave-uniform)
+#pragma unroll
+  for (int k = 1; k < kShards; ++k) pk[k] = __builtin_amdgcn_readlane(T.pre, b * kShards + k);
+  const int32_t j = w0 - bstart + lane;
   int32_t s = 0, off = j;
 #pragma unroll
   for (int k = 1; k < kShards; ++k) {
-    const int32_t pk = __builtin_amdgcn_readlane(T.pre, b * kShards + k);
-    if (j >= pk) {
+    if (j >= pk[k]) {
       s = k;
-      off = j - pk;
+      off = j - pk[k];
     }
   }
-  return (b * kShards + s) * wb.seg_cap + off;
+  return j < btot ? (b * kShards + s) * wb.seg_cap + off : -1;
 }
 
 // Direction bin of a continuing ray: its octant.
 __device__ __forceinline__ int32_t ray_bin(pt_v3 d) {
-  if constexpr (kBins == 1) {
-    return 0;
-  } else {
-    return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
-  }
+  return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
 }
 
 // Appends the wave's continuing rays to their segments of the next
@@ -608,149 +605,6 @@ __device__ __forceinline__ void append_list(const WfBufs& wb, int32_t par, int32
   if (list >= 0 && k < wb.medseg) s_store(list_slot(wb, list, shard, k), p);  // always < medseg: it bounds a shard's rays
 }
 
-#ifndef PTMI_WF_REFILL
-// 1: each wf_intersect wave works through a chunk of one section of the
-// work (a direction bin, the overflow region or the fresh rays) and refills
-// the lanes whose traversal has ended with the chunk's next rays, retiring
-// finished lanes (classification, list append) once at most
-// PTMI_WF_REFILL_AT lanes are still traversing — the megakernel's decoupled
-// step loop, on rays that are neighbours in their sorted segment. 0: one ray
-// per lane per 64-entry slice of the work.
-#define PTMI_WF_REFILL 0
-#endif
-#ifndef PTMI_WF_REFILL_AT
-#define PTMI_WF_REFILL_AT 16
-#endif
-#if PTMI_WF_REFILL
-// A lane's ray: continuing (position p of a segment or of the overflow
-// region) or fresh (item claimed, camera ray generated).
-template <int STACK, int TRAV, int LDS>
-__device__ __forceinline__ void wf_intersect_refill(const DevScene& sc, const DevFrame& fr, const WfBufs& wb,
-                                                    int32_t par, int32_t shard, const SegTable& T, int32_t nfresh,
-                                                    Stack st, uint32_t& n_live, uint32_t& n_ended) {
-  const RayBuf& X = wb.rb[par];
-  const int lane = lane_id();
-  // chunks: each bin's entries, the overflow entries and the fresh rays cut
-  // into pieces of ch entries (one piece per wave of the grid, about)
-  const int32_t waves = (int32_t)(gridDim.x * (kWfBlock / 64));
-  const int32_t total = T.live + nfresh;
-  const int32_t ch = max(64, ((total + waves - 1) / waves + 63) & ~63);
-  // lane b < kBins: chunks of bin b; then the overflow's and the fresh rays'
-  const int32_t nb = lane < kBins ? (T.btot + ch - 1) / ch : 0;
-  const int32_t nb_incl = wave_incl_scan(nb);
-  const int32_t bin_chunks = __shfl(nb_incl, 63);
-  const int32_t ovf_chunks = (T.ovf_n + ch - 1) / ch, fresh_chunks = (nfresh + ch - 1) / ch;
-  const int32_t nchunks = bin_chunks + ovf_chunks + fresh_chunks;
-  typename TravOf<TRAV>::T tr;
-  tr.init(st);
-  for (int32_t q = (int32_t)(blockIdx.x * (kWfBlock / 64) + (threadIdx.x >> 6)); q < nchunks; q += waves) {
-    // the chunk's section (wave-uniform): bin b, the overflow (-1) or the fresh rays (-2), and its entry range
-    int32_t b = -2, lo = 0, hi = 0;
-    if (q < bin_chunks) {
-      const unsigned long long m = pt_ballot(lane < kBins && nb_incl > q);
-      b = __ffsll((long long)m) - 1;
-      const int32_t first = __builtin_amdgcn_readlane(nb_incl, b) - __builtin_amdgcn_readlane(nb, b);
-      lo = (q - first) * ch;
-      hi = min(lo + ch, __builtin_amdgcn_readlane(T.btot, b));
-    } else if (q < bin_chunks + ovf_chunks) {
-      b = -1;
-      lo = (q - bin_chunks) * ch;
-      hi = min(lo + ch, T.ovf_n);
-    } else {
-      lo = (q - bin_chunks - ovf_chunks) * ch;
-      hi = min(lo + ch, nfresh);
-    }
-    int32_t cursor = lo;  // wave-uniform: the chunk's next entry
-    bool act = false;     // the lane holds a ray (traversing, or traced and not yet retired)
-    int32_t p = -1;
-    uint32_t item = 0u;
-    pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
-    for (;;) {
-      // refill the lanes without a ray from the chunk
-      const unsigned long long need = pt_ballot(!act);
-      if (need != 0ull && cursor < hi) {
-        const int32_t rank = (int32_t)lane_rank(need), n = (int32_t)__popcll(need);
-        const int32_t j = cursor + rank;
-        const bool take = !act && j < hi;
-        cursor = min(cursor + n, hi);
-        int32_t np = -1;
-        if (b >= 0 || b == -1) {
-          if (take) {
-            if (b == -1) {
-              np = ovf_base(wb) + j;
-            } else {
-              int32_t s = 0, off = j;
-#pragma unroll
-              for (int k = 1; k < kShards; ++k) {
-                const int32_t pk = __builtin_amdgcn_readlane(T.pre, b * kShards + k);
-                if (j >= pk) {
-                  s = k;
-                  off = j - pk;
-                }
-              }
-              np = (b * kShards + s) * wb.seg_cap + off;
-            }
-            item = s_load(X.item + np);
-            const float4 a = q_load(X.a + np);
-            const float2 dyz = h_load(X.d + np);
-            o = pt_v3f(a.x, a.y, a.z);
-            d = pt_v3f(a.w, dyz.x, dyz.y);
-          }
-        } else {  // generate_camera_rays (kernels.py:1219-1239) for the next work items
-          const int32_t k = claim_items(wb, shard, take);
-          if (k >= 0) {
-            const Item it = decode_item(fr, wb, (uint32_t)k);
-            if (it.valid) {
-              Rng rng{path_key(fr, wb, it), 0u};
-              get_ray(fr, it.px, it.py, rng, o, d);  // direction left unnormalized (Q1)
-              np = fresh_base(wb) + j;
-              item = (uint32_t)k | kFresh;
-              s_store(X.item + np, item);
-            }
-          }
-        }
-        if (np >= 0) {
-          p = np;
-          act = true;
-          ++n_live;
-          trav_begin<STACK, kWfBlock>(sc, tr, st, d, o, kTMin, kTMax);
-        }
-      }
-      if (pt_ballot(act) == 0ull) {
-        if (cursor >= hi) break;
-        continue;
-      }
-      // traversal steps until few lanes are still traversing
-      for (;;) {
-        const unsigned long long mbusy = pt_ballot(tr.busy());
-        const uint32_t nbusy = __builtin_popcount((uint32_t)mbusy) + __builtin_popcount((uint32_t)(mbusy >> 32));
-        if (nbusy == 0) break;
-        if (nbusy <= (uint32_t)PTMI_WF_REFILL_AT && pt_ballot(act && !tr.busy()) != 0ull) break;
-#pragma unroll
-        for (int u = 0; u < PTMI_TRAV_UNROLL; ++u)
-          if (tr.busy()) trav_step<STACK, kWfBlock, 0, LDS>(sc, sc.nodes, tr, st, o, d);
-      }
-      // retire the lanes whose traversal has ended: classify
-      const bool fin = act && !tr.busy();
-      int32_t list = -1;
-      if (fin) {
-        const int32_t ref = tr.any() ? tr.best : 0;  // 0: a miss
-        list = tr.any() ? leaf_class(ref) : kListEnded;
-        if (list == kListEnded) {
-          end_unscattered(sc, fr, wb, X, p, item, ref);
-          ++n_ended;
-          list = -1;
-        } else {
-          h_store(X.hit + p, make_float2(tr.closest, __int_as_float(ref)));
-        }
-        act = false;
-      }
-      append_list(wb, par, shard, list, p);
-    }
-  }
-}
-#endif
-
 // intersect_rays, kernels.py:1242-1263, plus the closest-hit classification:
 // a miss (shade_miss_rays, kernels.py:1266-1280) or an emissive hit
 // (kernels.py:1365-1375) ends its path here; every other traced ray is
@@ -761,13 +615,10 @@ __device__ __forceinline__ void wf_intersect_refill(const DevScene& sc, const De
 // lasts. Writes the hit record (8 B) and one list entry (4 B) per ray; a path
 // end reads thr (16 B) and writes its staging slot.
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-__global__ __launch_bounds__(kWfBlock, (isect_min_waves<STACK, TRAV>())) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
+__global__ __launch_bounds__(kWfBlock, stress_waves(isect_min_waves<STACK, TRAV>())) void wf_intersect(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                        unsigned long long* __restrict__ counters) {
   constexpr int LDS = isect_lds<STACK, TRAV>();
   __shared__ uint2 lds_stack[LDS * kWfBlock];
-#if PTMI_WF_PRIO_ISECT >= 0
-  __builtin_amdgcn_s_setprio(PTMI_WF_PRIO_ISECT);
-#endif
   const int tid = threadIdx.x;
   Stack st{lds_stack + tid, wb.spill, (uint32_t)(blockIdx.x * kWfBlock + tid) * 8u, gridDim.x * kWfBlock * 8u};
   const RayBuf& X = wb.rb[par];
@@ -785,11 +636,8 @@ __global__ __launch_bounds__(kWfBlock, (isect_min_waves<STACK, TRAV>())) void wf
     ctl_status(wb)[1] = dry ? 1 : 0;
   }
   uint32_t n_live = 0, n_ended = 0;
-#if PTMI_WF_REFILL
-  (void)stride;
-  wf_intersect_refill<STACK, TRAV, LDS>(sc, fr, wb, par, shard, T, nfresh, st, n_live, n_ended);
-#else
-  for (int32_t w0 = (int32_t)(blockIdx.x * kWfBlock) + (tid & ~63); w0 < nwork; w0 += stride) {
+  for (int32_t w0 = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * kWfBlock) + (tid & ~63)); w0 < nwork;
+       w0 += stride) {  // (wave-uniform: an SGPR)
     int32_t p = -1;
     uint32_t item = 0u;
     pt_v3 o = pt_v3f(0.0f, 0.0f, 0.0f), d = o;
@@ -834,7 +682,6 @@ __global__ __launch_bounds__(kWfBlock, (isect_min_waves<STACK, TRAV>())) void wf
     }
     append_list(wb, par, shard, list, p);
   }
-#endif
   if (counters) {
     block_flush<1>({n_live}, lds_stack, counters + 0);
     block_flush<1>({n_ended}, lds_stack, counters + 2);
@@ -1040,12 +887,9 @@ __device__ __forceinline__ void medium_entry(const DevScene& sc, const DevFrame&
 constexpr int32_t kScatterOrder[kLists] = {kListMedium, kListNoise, kListLambertian, kListGlossy, kListDielectric};
 
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-__global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatter(DevScene sc, DevFrame fr, WfBufs wb,
+__global__ __launch_bounds__(kWfBlock, stress_waves(PTMI_WF_SCATTER_MIN_WAVES)) void wf_scatter(DevScene sc, DevFrame fr, WfBufs wb,
                                                     int32_t par, unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
-#if PTMI_WF_PRIO_SCATTER >= 0
-  __builtin_amdgcn_s_setprio(PTMI_WF_PRIO_SCATTER);
-#endif
   Stack st{lds_stack + threadIdx.x};
   const RayBuf& X = wb.rb[par];
   const int32_t shard = (int32_t)(blockIdx.x % kShards);
@@ -1071,7 +915,8 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
   }
   const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
   uint32_t n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t base = (int32_t)(blockIdx.x * kWfBlock) + (int32_t)(threadIdx.x & ~63u); base < n; base += stride) {
+  for (int32_t base = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * kWfBlock) + (int32_t)(threadIdx.x & ~63u));
+       base < n; base += stride) {  // (wave-uniform: an SGPR)
     // wave-uniform list of this wave's 64 entries
     int32_t j = base + lane_id(), l = 0;
 #pragma unroll
@@ -1101,6 +946,91 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
   if (counters) block_flush<3>({n_ended, ends[0], ends[1]}, lds_stack, counters + 2);
 }
 
+#ifndef PTMI_WF_TRACE
+#define PTMI_WF_TRACE 0  // diagnostic builds only: record every wf_drain segment (tools/wf_drain_trace.py)
+#endif
+#if PTMI_WF_TRACE
+// One record per segment traced by wf_drain: item, meta and rng counter the
+// segment starts with, its closest hit (t, ref), then the continuation
+// (go, ctr, meta, thr.xyz) or, for an ended path, its staged colour.
+constexpr uint32_t kTraceWords = 12, kTraceCap = 1u << 22;
+__device__ uint32_t g_wf_trace_n;
+__device__ uint32_t g_wf_trace[kTraceCap * kTraceWords];
+#if PTMI_WF_TRACE == 1
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+void wf_trace(const DevFrame& fr, const WfBufs& wb, uint32_t item, uint32_t meta,
+                                      uint32_t ctr, float t, int32_t ref, uint32_t go, const Cont& cn) {
+  const uint32_t k = atomicAdd(&g_wf_trace_n, 1u);
+  if (k >= kTraceCap) return;
+  uint32_t* r = g_wf_trace + (size_t)k * kTraceWords;
+  r[0] = item;
+  r[1] = meta;
+  r[2] = ctr;
+  r[3] = __float_as_uint(t);
+  r[4] = (uint32_t)ref;
+  r[5] = go;
+  if (go) {
+    r[6] = cn.ctr;
+    r[7] = cn.meta;
+    r[8] = __float_as_uint(cn.thr.x);
+    r[9] = __float_as_uint(cn.thr.y);
+    r[10] = __float_as_uint(cn.thr.z);
+  } else {
+    const Item it = decode_item(fr, wb, item);
+    const float* c = wb.staging + 3 * ((size_t)it.srel * (size_t)wb.npix + (size_t)it.p);
+    r[6] = 0xffffffffu;
+    r[7] = 0xffffffffu;
+    r[8] = __float_as_uint(c[0]);
+    r[9] = __float_as_uint(c[1]);
+    r[10] = __float_as_uint(c[2]);
+  }
+  r[11] = 0x7ace0000u | (uint32_t)(threadIdx.x & 63);
+}
+#endif
+
+// One segment of a tail path at position p: intersect_rays (kernels.py:
+// 1242-1263), the classification of wf_intersect and the shading of
+// wf_scatter (the same entry functions); the continuing ray is stored back in
+// place. Returns whether the path goes on.
+template <int STACK, int TRAV>
+__device__ __forceinline__ bool drain_segment(const DevScene& sc, const DevFrame& fr, const WfBufs& wb, Stack st,
+                                              const RayBuf& X, int32_t p, uint32_t& n_seg, uint32_t& n_med,
+                                              uint32_t& n_ended, uint32_t (&ends)[2]) {
+  const float4 a = q_load(X.a + p);
+  const float2 dyz = h_load(X.d + p);
+#if PTMI_WF_TRACE
+  const uint32_t tr_item = s_load(X.item + p), tr_meta = __float_as_uint(q_load(X.c + p).w),
+                 tr_ctr = s_load(X.ctr + p);
+#endif
+  float t = 0.0f;
+  int32_t ref = 0;
+  const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, pt_v3f(a.x, a.y, a.z), pt_v3f(a.w, dyz.x, dyz.y), kTMin,
+                                                   kTMax, st, t, ref);
+  ++n_seg;
+  if (!hit) ref = 0;
+  h_store(X.hit + p, make_float2(t, __int_as_float(ref)));
+  const int32_t list = hit ? leaf_class(ref) : kListEnded;
+  Cont cn;
+  cn.go = false;
+  if (list == kListEnded) {
+    end_unscattered(sc, fr, wb, X, p, s_load(X.item + p), ref);
+    ++n_ended;
+  } else if (list == kListMedium || list == kListNoise) {
+    n_med += list == kListMedium ? 1u : 0u;
+    medium_entry<STACK, TRAV>(sc, fr, wb, st, X, p, list == kListNoise, n_ended, ends, cn);
+  } else {
+    shade_entry(sc, fr, wb, X, list, p, n_ended, ends, cn);
+  }
+#if PTMI_WF_TRACE
+  wf_trace(fr, wb, tr_item, tr_meta, tr_ctr, t, ref, cn.go ? 1u : 0u, cn);
+#endif
+  if (cn.go) store_ray(X, p, cn);
+  return cn.go;  // false: the path ended (its colour is staged)
+}
+
 // The tail of a batch (wf_batch switches a pipe to it once the work pool is
 // empty and the pipe traces fewer than capacity / drain_at rays per
 // iteration): one launch finishes every path still in the pipe, each lane
@@ -1114,45 +1044,25 @@ __global__ __launch_bounds__(kWfBlock, PTMI_WF_SCATTER_MIN_WAVES) void wf_scatte
 // whose length is the longest remaining path. Launched on the pipe's stream
 // after a wf_scatter, on the continuing rays of the next iteration's parity:
 // the pool is empty, so no fresh ray is due.
+#ifndef PTMI_WF_DRAIN_MIN_WAVES
+#define PTMI_WF_DRAIN_MIN_WAVES 1
+#endif
 template <int STACK, int TRAV = PTMI_TRAV_STACK>
-__global__ __launch_bounds__(kWfBlock) void wf_drain(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
+__global__ __launch_bounds__(kWfBlock, stress_waves(PTMI_WF_DRAIN_MIN_WAVES)) void wf_drain(DevScene sc, DevFrame fr, WfBufs wb, int32_t par,
                                                    unsigned long long* __restrict__ counters) {
   __shared__ uint2 lds_stack[STACK * kWfBlock];
   Stack st{lds_stack + threadIdx.x};
   const RayBuf& X = wb.rb[par];
   const SegTable T = seg_table(wb, par);
   uint32_t n_seg = 0, n_med = 0, n_ended = 0, ends[2] = {0u, 0u};
-  for (int32_t w0 = (int32_t)(blockIdx.x * kWfBlock) + (int32_t)(threadIdx.x & ~63u); w0 < T.fresh_start;
-       w0 += (int32_t)(gridDim.x * kWfBlock)) {
-    const int32_t p = cont_position(T, wb, w0);
+  // (the wave's work index is wave-uniform: an SGPR)
+  const int32_t stride = (int32_t)(gridDim.x * kWfBlock);
+  for (int32_t w0 = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * kWfBlock) + (int32_t)(threadIdx.x & ~63u));
+       w0 < T.fresh_start; w0 += stride) {
+    const int32_t p = cont_position(T, wb, w0);  // (every lane active: cross-lane reads inside)
     if (p < 0) continue;
-    for (;;) {
-      // intersect_rays (kernels.py:1242-1263) for this ray
-      const float4 a = q_load(X.a + p);
-      const float2 dyz = h_load(X.d + p);
-      float t = 0.0f;
-      int32_t ref = 0;
-      const bool hit = traverse<STACK, kWfBlock, TRAV>(sc, pt_v3f(a.x, a.y, a.z), pt_v3f(a.w, dyz.x, dyz.y), kTMin,
-                                                       kTMax, st, t, ref);
-      ++n_seg;
-      if (!hit) ref = 0;
-      h_store(X.hit + p, make_float2(t, __int_as_float(ref)));
-      const int32_t list = hit ? leaf_class(ref) : kListEnded;
-      if (list == kListEnded) {
-        end_unscattered(sc, fr, wb, X, p, s_load(X.item + p), ref);
-        ++n_ended;
-        break;
-      }
-      Cont cn;
-      cn.go = false;
-      if (list == kListMedium || list == kListNoise) {
-        n_med += list == kListMedium ? 1u : 0u;
-        medium_entry<STACK, TRAV>(sc, fr, wb, st, X, p, list == kListNoise, n_ended, ends, cn);
-      } else {
-        shade_entry(sc, fr, wb, X, list, p, n_ended, ends, cn);
-      }
-      if (!cn.go) break;  // the path ended (its colour is staged)
-      store_ray(X, p, cn);
+    // each lane loops over its own path until it ends
+    while (drain_segment<STACK, TRAV>(sc, fr, wb, st, X, p, n_seg, n_med, n_ended, ends)) {
     }
   }
   if (counters) {
@@ -1379,6 +1289,29 @@ static hipError_t wf_batch(const DevScene& sc, const DevFrame& fr, const WfBufs*
 }
 
 int32_t wf_set_drain_at(int32_t divisor) { return g_drain_at.exchange(divisor); }
+
+#if PTMI_WF_TRACE
+}  // namespace ptmi
+// Diagnostic builds: copy up to max_records wf_drain segment records to out
+// (kTraceWords uint32 each) and return how many were recorded; reset clears.
+extern "C" int64_t ptmi_wf_trace_read(uint32_t* out, int64_t max_records, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  uint32_t n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(ptmi::g_wf_trace_n), sizeof(n)) != hipSuccess) return -1;
+  const int64_t k = (int64_t)(n < ptmi::kTraceCap ? n : ptmi::kTraceCap);
+  const int64_t m = k < max_records ? k : max_records;
+  if (m > 0 && out &&
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi::g_wf_trace), (size_t)m * ptmi::kTraceWords * sizeof(uint32_t)) !=
+          hipSuccess)
+    return -1;
+  if (reset) {
+    n = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ptmi::g_wf_trace_n), &n, sizeof(n)) != hipSuccess) return -1;
+  }
+  return (int64_t)n;
+}
+namespace ptmi {
+#endif
 
 size_t wf_workspace_bytes(int32_t npix, int32_t batch) {
   if (npix <= 0 || batch <= 0) return 0;

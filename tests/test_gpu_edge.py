@@ -115,7 +115,7 @@ def test_stack_overflow_drops_match_the_oracle(variant, spp):
 @pytest.mark.parametrize('variant', ['mk', 'wf'])
 def test_leaf_depth_16_to_19_exact_slot_kernels(name, variant):
     # leaf depth 16-18: the staged megakernel's 17-, 18- and 19-slot kernels
-    # (PTMI_MK_EXACT_STACK); 19: its 20-slot kernel; the wavefront's 20-slot ones
+    # (exact-stack kernels 17-19); 19: its 20-slot kernel; the wavefront's 20-slot ones
     from ptmi import scene_data as sd
     depth = sd.pack_device(edge_scene(name)[0]).max_leaf_depth
     assert depth == int(name[5:]) - 1

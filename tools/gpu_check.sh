@@ -23,6 +23,8 @@
 #                         (<lib> = default: the default build)
 #   abpmc_<lib>_<mk|wf>   FETCH_SIZE, WRITE_SIZE and cache-hit PMC passes of tools/ab.py (32 spp x 1), same libs
 #   ablat_<lib>_<mk|wf>   the VALU / wait PMC passes (tools/gpu_pmc_latency.sh) with variants/libptmi_<lib>.so
+#   drainbug              tools/gpu_drain_bug.sh: wavefront parity windows at two tail thresholds per build
+#                         (DRAIN_LIBS, default "dr5 tr5 tr3": the 5-wave wf_drain and the trace builds)
 #   probe                 the diagnostic probe builds (tools/gpu_probe.sh; variants libptmi_probe{1,2}.so)
 #   abbench_<c>           bench.py --preset <c> (no CPU baseline) for the default build and every variants/*.so
 #                         (MK_VARIANTS: only those), two interleaved rounds -> OUT/abbench_<c>.txt
@@ -69,6 +71,7 @@ for s in $STEPS; do
     latc4_mk|latc4_wf) v=${s#latc4_}; step $s 600 env PMC_VARIANT=$v PMC_DIR=$OUT/pmc_latency_c4_$v PMC_SCENE_ARGS="cornell_mesh_fog 1024" bash tools/gpu_pmc_latency.sh ;;
     latc5_mk) step $s 600 env PMC_VARIANT=mk PMC_DIR=$OUT/pmc_latency_c5_mk PMC_SCENE_ARGS="vol2_final_scene_comparison 3840" bash tools/gpu_pmc_latency.sh ;;
     probe) step probe 600 bash tools/gpu_probe.sh ;;
+    drainbug) step drainbug 1200 env LIBS="${DRAIN_LIBS:-dr5 tr5 tr3}" STEP_S=300 bash tools/gpu_drain_bug.sh ;;
     abbench_*) c=${s#abbench_}; libs=(path-tracer-python_amd/ptmi/_lib/libptmi.so)
       if [ -n "${MK_VARIANTS:-}" ]; then for n in $MK_VARIANTS; do libs+=(path-tracer-python_amd/ptmi/_lib/variants/libptmi_$n.so); done
       else libs+=(path-tracer-python_amd/ptmi/_lib/variants/*.so); fi
