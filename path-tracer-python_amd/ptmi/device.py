@@ -38,11 +38,9 @@ class DeviceScene:
     def __init__(self, scene, device=None):
         require_gpu()
         node_bytes = int(_lib.load().ptmi_node_bytes())
-        # PTMI_PACK_LEAF_ORDER=0: compile-order primitives; PTMI_NODE_ORDER:
-        # node placement (scene_data.NODE_ORDERS). A/B timing only: same results
+        # PTMI_PACK_LEAF_ORDER=0: compile-order primitives (A/B timing only: same results)
         leaf_order = os.environ.get('PTMI_PACK_LEAF_ORDER', '1') != '0'
-        node_order = os.environ.get('PTMI_NODE_ORDER', 'preorder')
-        layout = scene if isinstance(scene, DeviceLayout) else pack_device(scene, node_bytes, leaf_order, node_order)
+        layout = scene if isinstance(scene, DeviceLayout) else pack_device(scene, node_bytes, leaf_order)
         if layout.n_inner and layout.nodes.shape[1] * 4 != node_bytes:
             raise _lib.PtmiError(f'scene packed with {layout.nodes.shape[1] * 4}-B nodes, '
                                  f'libptmi expects {node_bytes}')

@@ -183,16 +183,9 @@ CLASS_LAMBERTIAN, CLASS_GLOSSY, CLASS_DIELECTRIC, CLASS_MEDIUM, CLASS_NOISE, CLA
 
 NODE_FLOATS = 20  # 80-B internal node (include/ptmi.h)
 NODE_BYTES = 4 * NODE_FLOATS  # an internal child ref is the child's byte offset in the node array
-# Node strides a library build may use (ptmi_node_bytes()): 80 (both
-# children's x / y centres stored in the last 16 B, not read) or 64 (without
-# them: the kernels compute them from the boxes either way).
-NODE_STRIDES = (64, 80)
-# Placement of the internal nodes in the node array (refs are byte offsets,
-# so any placement walks the same tree in the same order): the reference's
-# preorder; breadth first (a node's two internal children adjacent); or
-# "pairs", depth first over sibling pairs (children adjacent, each subtree
-# contiguous). With 64-B nodes the pairs start on 128-B lines.
-NODE_ORDERS = ('preorder', 'bfs', 'pairs')
+# Internal nodes sit in the node array in the reference's preorder. (A/B,
+# rounds 1, 4 and 5, not kept: a 64-B stride without the stored x / y centres,
+# breadth-first and depth-first sibling-pair placements; profiles/HISTORY.md §9d.)
 
 
 def leaf_code(prim_type, prim_idx, mat_class=0):
@@ -355,39 +348,16 @@ def ref_layout_nodes(bvh, codes):
     return out
 
 
-def node_slots(left, right, is_leaf, order='preorder', align_pairs=False):
+def node_slots(left, right, is_leaf):
     """Slot (row of the node array) of every internal node, by reference node
-    index (-1 for leaves), and the number of rows (NODE_ORDERS). align_pairs:
-    two internal siblings start on an even row (a 128-B line of 64-B nodes);
-    a skipped row is padding no ref points to."""
-    n = left.shape[0]
-    internal = ~is_leaf
-    slot = np.full(n, -1, np.int64)
-    if order not in NODE_ORDERS:
-        raise ValueError(f'unknown node order {order!r} (one of {NODE_ORDERS})')
-    if order == 'preorder' or n == 0 or not internal[0]:
-        idx = np.nonzero(internal)[0]
-        slot[idx] = np.arange(idx.shape[0])
-        return slot, int(idx.shape[0])
-
-    def kids(i):
-        return [int(c) for c in (left[i], right[i]) if c >= 0 and internal[c]]
-    slot[0], k = 0, 1
-    todo = collections.deque([0])
-    while todo:
-        i = todo.popleft() if order == 'bfs' else todo.pop()
-        ch = kids(i)
-        if align_pairs and len(ch) == 2 and k % 2:
-            k += 1
-        for c in ch:
-            slot[c] = k
-            k += 1
-        todo.extend(ch if order == 'bfs' else reversed(ch))  # pairs: the left subtree first
-    return slot, k
+    index (-1 for leaves), in the reference's preorder, and the number of rows."""
+    slot = np.full(left.shape[0], -1, np.int64)
+    idx = np.nonzero(~is_leaf)[0]
+    slot[idx] = np.arange(idx.shape[0])
+    return slot, int(idx.shape[0])
 
 
-def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True,
-                node_order: str = 'preorder') -> DeviceLayout:
+def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool = True) -> DeviceLayout:
     """Reference-layout arrays -> include/ptmi.h device layout. ``node_bytes``
     is the library's node stride (ptmi_node_bytes(): 80, one child record
     per internal node). Each leaf code carries its primitive's material
@@ -433,9 +403,9 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
         cls = np.where(is_leaf, material_class(mats[rows, 19].view(np.uint32)) if len(mats) else 0, 0)
     codes = ((LEAF_FLAG | (ptype.astype(np.int64) << 28) | (cls << LEAF_INDEX_BITS) | new_idx)
              - (1 << 32)).astype(np.int32)
-    if node_bytes not in NODE_STRIDES:
-        raise ValueError(f'unsupported node stride {node_bytes}')
-    cidx, nrows = node_slots(left, right, is_leaf, node_order, align_pairs=node_bytes == 64)
+    if node_bytes != NODE_BYTES:
+        raise ValueError(f'unsupported node stride {node_bytes} (the library reads {NODE_BYTES}-B nodes)')
+    cidx, nrows = node_slots(left, right, is_leaf)
     if nrows * node_bytes > 0x7fffffff:
         raise ValueError(f'{nrows} BVH node rows: byte offsets exceed int32')
     refs = np.where(is_leaf, codes, (cidx * node_bytes).astype(np.int32)).astype(np.int32)
@@ -452,9 +422,8 @@ def pack_device(sa: SceneArrays, node_bytes: int = NODE_BYTES, leaf_order: bool 
         cl = (bmin[l] + bmax[l]) * np.float32(0.5)
         cr = (bmin[r] + bmax[r]) * np.float32(0.5)
         nodes[rows, 14], nodes[rows, 15] = cl[:, 2], cr[:, 2]
-        if node_bytes == 80:
-            nodes[rows, 16], nodes[rows, 17] = cl[:, 0], cr[:, 0]
-            nodes[rows, 18], nodes[rows, 19] = cl[:, 1], cr[:, 1]
+        nodes[rows, 16], nodes[rows, 17] = cl[:, 0], cr[:, 0]
+        nodes[rows, 18], nodes[rows, 19] = cl[:, 1], cr[:, 1]
     ref_nodes = ref_layout_nodes(b, np.where(is_leaf, codes, 0).astype(np.int32))
     if n:
         root_ref = int(refs[0])

@@ -1,49 +1,62 @@
-"""CPU: the node array's placement (scene_data.NODE_ORDERS, PTMI_NODE_ORDER)
-and stride (64 / 80 B) change where nodes sit, never the tree the kernels
-walk: from the root ref, every placement reaches the same boxes, refs
-resolved, in the same depth-first order (so the traversal, which follows
-refs, visits the same nodes in the same order)."""
+"""CPU: the packed node array walks the reference's tree: from the root ref,
+following refs (byte offsets of 80-B nodes), the walk reaches every internal
+node's two child boxes and every leaf in the reference's depth-first order.
+Other strides and placements are refused."""
 import numpy as np
 import pytest
 
 from ptmi import scene_data as sd
 
 
-def _walk(L, node_bytes):
+def _walk(L):
     out, stack = [], [L.root_ref]
     while stack:
         r = stack.pop()
         if r < 0:
             out.append(('leaf', int(r)))
             continue
-        assert r % node_bytes == 0
-        row = L.nodes[r // node_bytes]
+        assert r % sd.NODE_BYTES == 0
+        row = L.nodes[r // sd.NODE_BYTES]
         out.append(tuple(np.asarray(row[:12]).tolist()) + (float(row[14]), float(row[15])))
         refs = row[12:14].view(np.int32)
         stack.extend([int(refs[1]), int(refs[0])])
     return out
 
 
+def _ref_walk(sa):
+    """The same walk over the reference's own BVH arrays."""
+    b = sa.bvh
+    left, right, pidx = b['bvh_left_child'], b['bvh_right_child'], b['bvh_prim_idx']
+    out, stack = [], [0]
+    while stack:
+        i = stack.pop()
+        if pidx[i] >= 0:
+            out.append('leaf')
+            continue
+        l, r = int(left[i]), int(right[i])
+        out.append(tuple(np.concatenate([np.stack([b['bvh_bbox_min'][l], b['bvh_bbox_min'][r]], 1).ravel(),
+                                         np.stack([b['bvh_bbox_max'][l], b['bvh_bbox_max'][r]], 1).ravel()]).tolist()))
+        stack.extend([r, l])
+    return out
+
+
 @pytest.mark.parametrize('name', ['vol2_final_scene', 'wavefront_comparison', 'cornell_smoke'])
-def test_every_placement_walks_the_same_tree(name):
+def test_node_array_walks_the_reference_tree(name):
     sa = sd.load_fixture(name)
-    base = sd.pack_device(sa)
-    want = _walk(base, 80)
-    for nb in sd.NODE_STRIDES:
-        for order in sd.NODE_ORDERS:
-            L = sd.pack_device(sa, nb, True, order)
-            assert L.n_inner == base.n_inner == sd.pack_device(sa).nodes.shape[0]
-            assert L.nodes.shape[1] * 4 == nb
-            assert _walk(L, nb) == want, (nb, order)
-            if nb == 64 and order == 'pairs':  # two internal siblings share one 128-B line
-                refs = L.nodes[:, 12:14].view(np.int32)
-                both = (refs[:, 0] >= 0) & (refs[:, 1] >= 0)
-                assert np.array_equal(refs[both, 0] // 128, refs[both, 1] // 128)
+    L = sd.pack_device(sa)
+    got = _walk(L)
+    want = _ref_walk(sa)
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        if w == 'leaf':
+            assert g[0] == 'leaf'
+        else:  # boxes interleaved per component: min.x L,R, min.y L,R, ..., max.z L,R
+            assert g[:12] == w
 
 
-def test_unknown_order_and_stride_are_refused():
+def test_unknown_stride_is_refused():
     sa = sd.load_fixture('cornell_smoke')
     with pytest.raises(ValueError):
-        sd.pack_device(sa, 80, True, 'random')
+        sd.pack_device(sa, 64)
     with pytest.raises(ValueError):
         sd.pack_device(sa, 96)

@@ -25,7 +25,7 @@ def main():
     best = 1e9
     for r in range(reps):
         t = time.perf_counter(); f(fr, acc, 4 + r * spp, spp); torch.cuda.synchronize(); best = min(best, time.perf_counter() - t)
-    print(json.dumps({'lib': os.path.basename(_lib.LIB_PATH), 'node_order': os.environ.get('PTMI_NODE_ORDER', 'preorder'),
+    print(json.dumps({'lib': os.path.basename(_lib.LIB_PATH),
                       'variant': variant, 'scene': scene, 'width': width,
                       'spp': spp, 'Msamples_s': round(W * H * spp / best / 1e6, 1), 'ms': round(best * 1e3, 2)}),
           flush=True)
