@@ -2,7 +2,7 @@
 # Fold one counter re-collection (not product) into profiles/: the output of
 #   bash tools/gpu_check.sh OUT trace_c2 trace_c3 fetch_c2 write_c2 fetch_c3 write_c3 \
 #     fetch_c4 write_c4 fetch_c5 write_c5 lat_mk lat_wf latc4_mk latc5_mk ta_mk ta_wf cache_mk cache_wf
-# merged back under gpurun_out/OUT is compressed into profiles/r05/{pmc_final,rocprof}/
+# merged back under gpurun_out/OUT is compressed into profiles/$ROUND/{pmc_final,rocprof}/ (ROUND: r06)
 # and profiles/traffic.json, profiles/valu.json, the TA / cache summaries and the
 # trace busy figures are regenerated, every row naming HASH (the last commit that
 # touched the kernel sources). Usage: bash tools/refresh_counters.sh OUT
@@ -10,8 +10,10 @@ set -eu
 cd "$(dirname "$0")/.."
 SRC=gpurun_out/$1
 HASH=$(git log -1 --format=%h -- path-tracer-python_amd/csrc include)
-P=profiles/r05/pmc_final
-R=profiles/r05/rocprof
+ROUND=${ROUND:-r06}
+P=profiles/$ROUND/pmc_final
+R=profiles/$ROUND/rocprof
+mkdir -p "$P" "$R"
 for c in c2 c3 c4 c5; do
   for k in fetch write; do gzip -9nc "$SRC/pmc/${k}_${c}_counter_collection.csv" > "$P/${k}_${c}_counter_collection.csv.gz"; done
 done
@@ -31,7 +33,7 @@ TMP=$(mktemp -d)
 z() { gunzip -c "$1" > "$TMP/$(basename "$1" .gz)"; echo "$TMP/$(basename "$1" .gz)"; }
 traffic() {  # key kernel preset
   python3 tools/pmc_traffic.py "$1" "$2" "$(z $P/fetch_$3_counter_collection.csv.gz)" "$(z $P/write_$3_counter_collection.csv.gz)" \
-    "$P/{fetch,write}_$3_counter_collection.csv.gz (round 5 HEAD $HASH; bench.py --preset $3 --steps 4 --no-cpu-baseline under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"
+    "$P/{fetch,write}_$3_counter_collection.csv.gz ($ROUND HEAD $HASH; bench.py --preset $3 --steps 4 --no-cpu-baseline under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"
 }
 traffic vol2_final_scene:800:mk:64:50:megakernel mk_render_kernel c2
 traffic vol2_final_scene:800:wf:64:50:wf_intersect wf_intersect c3
@@ -43,7 +45,7 @@ traffic vol2_final_scene_comparison:3840:mk:16:50:megakernel mk_render_kernel c5
 valu() {  # key dir prefix kernel scene
   local d=$TMP/$2; mkdir -p "$d"
   for f in $P/$2/*_counter_collection.csv.gz; do gunzip -c "$f" > "$d/$(basename "$f" .gz)"; done
-  PMC_SOURCE="$P/$2/$3_{a,b,c}_counter_collection.csv.gz (round 5 HEAD $HASH; tools/gpu_pmc_latency.sh: tools/ab.py $3 32 1, one 32-spp call on $5; kernel $4); tools/pmc_valu.py" \
+  PMC_SOURCE="$P/$2/$3_{a,b,c}_counter_collection.csv.gz ($ROUND HEAD $HASH; tools/gpu_pmc_latency.sh: tools/ab.py $3 32 1, one 32-spp call on $5; kernel $4); tools/pmc_valu.py" \
     python3 tools/pmc_valu.py "$1" "$d" "$3" "$4"
 }
 valu vol2_final_scene:800:mk:megakernel pmc_latency_mk mk mk_render_kernel "vol2_final_scene 800"
