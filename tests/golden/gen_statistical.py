@@ -28,6 +28,11 @@ against these, within the standard errors of both.
                  Q9) and an image-textured sphere (the earthmap, sphere UV +
                  v flip, sphere.py:72-82, texture.py:66-79 / Q8, Q30), seen
                  through a defocus camera (camera.py:64-67, 128-131);
+  * mesh       — the same open quad box and light around a Lambertian
+                 octahedron and a mirror (fuzz 0) tetrahedron: triangles
+                 (core/triangle.py, Moller-Trumbore, normal flipped toward the
+                 ray as the kernels do, Q2 / Q18) in a composed render, the
+                 triangle half of C4's cornell_mesh_fog;
   * medium     — an isolated constant-medium sphere (nothing inside it)
                  against the sky and an emissive sphere. The two integrators
                  agree on the first free-flight segment only: entry at the
@@ -104,6 +109,21 @@ SCENES = {
             [[-0.6, 2.38, -0.7], [1.2, 0.0, 0.0], [0.0, 0.0, 1.0], ['diffuse_light', [6.0, 6.0, 6.0]]],  # light
         ],
     },
+    # triangles: a Lambertian octahedron and a mirror (fuzz 0) tetrahedron in
+    # the open quad box under the quad light (the mesh half of C4's scene)
+    'mesh': {
+        'width': 32, 'aspect': 16.0 / 9.0, 'vfov': 40.0, 'lookfrom': [0.0, 1.0, 4.2], 'lookat': [0.0, 0.9, 0.0],
+        'vup': [0.0, 1.0, 0.0], 'background': [0.0, 0.0, 0.0], 'max_depth': 50,
+        'quads': [
+            [[-2.0, 0.0, -1.5], [4.0, 0.0, 0.0], [0.0, 0.0, 3.5], ['lambertian', [0.7, 0.7, 0.7]]],   # floor
+            [[-2.0, 0.0, -1.5], [0.0, 2.4, 0.0], [4.0, 0.0, 0.0], ['lambertian', [0.6, 0.6, 0.65]]],  # back
+            [[-2.0, 0.0, -1.5], [0.0, 0.0, 3.5], [0.0, 2.4, 0.0], ['lambertian', [0.65, 0.1, 0.1]]],  # left
+            [[2.0, 0.0, -1.5], [0.0, 2.4, 0.0], [0.0, 0.0, 3.5], ['lambertian', [0.12, 0.5, 0.15]]],  # right
+            [[-2.0, 2.4, -1.5], [4.0, 0.0, 0.0], [0.0, 0.0, 3.5], ['lambertian', [0.7, 0.7, 0.7]]],   # ceiling
+            [[-0.6, 2.38, -0.7], [1.2, 0.0, 0.0], [0.0, 0.0, 1.0], ['diffuse_light', [6.0, 6.0, 6.0]]],  # light
+        ],
+        'triangles': [],  # filled below: v0, v1, v2, material
+    },
     # isolated constant-medium sphere against the sky and an emissive sphere
     'medium': {
         'width': 32, 'aspect': 16.0 / 9.0, 'vfov': 34.0, 'lookfrom': [0.0, 0.3, 4.0], 'lookat': [0.0, 0.0, 0.0],
@@ -116,6 +136,25 @@ SCENES = {
         ],
     },
 }
+
+
+def _solids():
+    """The 'mesh' scene's triangles: an octahedron (8) and a tetrahedron (4),
+    counter-clockwise seen from outside."""
+    tris = []
+    c, r = (-0.6, 0.5, -0.2), 0.45
+    px, nx, py, ny, pz, nz = ([c[0] + r, c[1], c[2]], [c[0] - r, c[1], c[2]], [c[0], c[1] + r, c[2]],
+                              [c[0], c[1] - r, c[2]], [c[0], c[1], c[2] + r], [c[0], c[1], c[2] - r])
+    for a, b, t in ((px, py, pz), (py, nx, pz), (nx, ny, pz), (ny, px, pz),
+                    (py, px, nz), (nx, py, nz), (ny, nx, nz), (px, ny, nz)):
+        tris.append([a, b, t, ['lambertian', [0.75, 0.55, 0.2]]])
+    v = [[0.65, 0.9, 0.1], [0.25, 0.02, -0.15], [1.05, 0.02, -0.15], [0.65, 0.02, 0.55]]
+    for a, b, t in ((1, 3, 2), (0, 1, 2), (0, 2, 3), (0, 3, 1)):
+        tris.append([v[a], v[b], v[t], ['metal', [0.85, 0.85, 0.9]]])
+    return tris
+
+
+SCENES['mesh']['triangles'] = _solids()
 SPP = 4096
 NAME = 'lambert'
 
@@ -150,6 +189,7 @@ def _build():
     from core.constant_medium import constant_medium  # noqa: E402
     from core.material import lambertian  # noqa: E402
     from core.quad import quad  # noqa: E402
+    from core.triangle import triangle  # noqa: E402
     from util import color, point3, vec3  # noqa: E402
     SCENE = SCENES[NAME]
     world = hittable_list()
@@ -157,6 +197,8 @@ def _build():
         world.add(Sphere.stationary(point3(*c), r, _material(spec)))
     for q, u, v, spec in SCENE.get('quads', []):
         world.add(quad(point3(*q), vec3(*u), vec3(*v), _material(spec)))
+    for v0, v1, v2, spec in SCENE.get('triangles', []):
+        world.add(triangle(point3(*v0), point3(*v1), point3(*v2), _material(spec)))
     for c, r, density, albedo in SCENE.get('media', []):
         boundary = Sphere.stationary(point3(*c), r, lambertian.from_color(color(0.5, 0.5, 0.5)))
         world.add(constant_medium.from_color(boundary, color(*albedo), density))

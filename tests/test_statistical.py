@@ -1,11 +1,12 @@
 """Statistical pin of the oracle against the reference's own integrator.
 
 tests/golden/stat_<scene>.npz hold per-pixel means and variances of the
-reference's pure-Python path tracer (core/camera.py ray_color, 4096 spp) on four
+reference's pure-Python path tracer (core/camera.py ray_color, 4096 spp) on five
 scenes (tests/golden/gen_statistical.py, which documents each): all-Lambertian
 spheres under a sky; glass / mirror / Lambertian spheres lit by an emissive
 sphere; an open box of Lambertian quads lit by a quad light with a checker-
-and an image-textured sphere through a defocus camera; and an isolated
+and an image-textured sphere through a defocus camera; the same box around a
+Lambertian octahedron and a mirror tetrahedron (triangles); and an isolated
 constant-medium sphere (first free-flight segment: density, exit search,
 transmittance). The same scene built
 from ptmi.core, compiled (compile_scene + native SAH) and rendered by the C
@@ -32,7 +33,7 @@ import pytest
 import oracle
 from ptmi import scene_data as sd
 from ptmi.core import (Sphere, camera, checker_texture, color, constant_medium, dielectric, diffuse_light,
-                       hittable_list, image_texture, lambertian, metal, point3, quad, vec3)
+                       hittable_list, image_texture, lambertian, metal, point3, quad, triangle, vec3)
 from ptmi.scenes import _wrap
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
@@ -63,6 +64,8 @@ def _scene(name):
         w.add(Sphere.stationary(point3(*c), r, _material(spec)))
     for q, u, v, spec in sc.get('quads', []):
         w.add(quad(point3(*q), vec3(*u), vec3(*v), _material(spec)))
+    for v0, v1, v2, spec in sc.get('triangles', []):
+        w.add(triangle(point3(*v0), point3(*v1), point3(*v2), _material(spec)))
     for c, r, density, albedo in sc.get('media', []):
         boundary = Sphere.stationary(point3(*c), r, lambertian.from_color(color(0.5, 0.5, 0.5)))
         w.add(constant_medium.from_color(boundary, color(*albedo), density))
@@ -80,7 +83,7 @@ def _scene(name):
     return sc, world, cam
 
 
-SCENES = ['lambert', 'materials', 'quads', 'medium']
+SCENES = ['lambert', 'materials', 'quads', 'mesh', 'medium']
 
 
 def oracle_stats(name, perturb=None):
