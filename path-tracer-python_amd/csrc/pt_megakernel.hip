@@ -169,6 +169,14 @@ constexpr int kMkBlock = 64;
 #ifndef PTMI_MK_SMALL_BATCH
 #define PTMI_MK_SMALL_BATCH 8000000
 #endif
+#ifndef PTMI_MK_SMALL_WPC
+// Persistent waves per CU for a batch of fewer than PTMI_MK_SMALL_BATCH
+// samples (the occupancy allows 20 for vol2). A/B on MI355X (round 5): 10 / 14
+// / 17 waves per CU against 20, an 8-rank tile shard's 64-spp call +1.2 / +1.0
+// / +0.6 %, whole frame at 8 spp +1.2 / +1.0 / +0.4 %, at 64 spp -1.1 / -0.3 /
+// +0.1 % (profiles/r05/ab/ab_mk_persist_wpc.log).
+#define PTMI_MK_SMALL_WPC 10
+#endif
 #ifndef PTMI_MK_TAIL_DIV
 #define PTMI_MK_TAIL_DIV 4  // a fetch takes at most (units left) / (TAIL_DIV * waves) units
                             // (re-tuned: 2 is +3 % on C2 but -8 % on C4's long fog paths;
@@ -781,9 +789,9 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   wk.by_len = fast_div((uint32_t)wk.shard_len);
   wk.by_nb = fast_div((uint32_t)nb);
   wk.by_tiles_x = fast_div((uint32_t)wk.tiles_x);
-#ifdef PTMI_MK_PERSIST_WPC
-  per_cu = PTMI_MK_PERSIST_WPC;
-#endif
+  // Small batches (an 8-rank tile shard) run on a smaller persistent grid, so
+  // the next overlapped call's waves share the chip while this one drains.
+  if ((int64_t)fr.w * fr.n_rows * nb < PTMI_MK_SMALL_BATCH && per_cu > PTMI_MK_SMALL_WPC) per_cu = PTMI_MK_SMALL_WPC;
   int64_t waves = (int64_t)(per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
   const int64_t chunks = wk.nunits;
   if (waves > chunks) waves = chunks;
