@@ -170,12 +170,20 @@ constexpr int kMkBlock = 64;
 #define PTMI_MK_SMALL_BATCH 8000000
 #endif
 #ifndef PTMI_MK_SMALL_WPC
-// Persistent waves per CU for a batch of fewer than PTMI_MK_SMALL_BATCH
-// samples (the occupancy allows 20 for vol2). A/B on MI355X (round 5): 10 / 14
-// / 17 waves per CU against 20, an 8-rank tile shard's 64-spp call +1.2 / +1.0
-// / +0.6 %, whole frame at 8 spp +1.2 / +1.0 / +0.4 %, at 64 spp -1.1 / -0.3 /
-// +0.1 % (profiles/r05/ab/ab_mk_persist_wpc.log).
+// Persistent waves per CU for a batch of fewer than PTMI_MK_SMALL_GRID_BATCH
+// samples (the occupancy allows 20 for vol2): the next overlapped call's waves
+// share the chip while this one drains. A/B on MI355X, an 8-rank tile shard's
+// 64-spp calls against 20 waves per CU: 10 +1.1 %, 12 +0.6 %, 14 +0.5 %, 16
+// -0.6 %, 8 -4 %, 6 -29 % (profiles/r06/ab/mk_small_grid.log; round 5:
+// profiles/r05/ab/ab_mk_persist_wpc.log).
 #define PTMI_MK_SMALL_WPC 10
+#endif
+#ifndef PTMI_MK_SMALL_GRID_BATCH
+// Batches (samples) below which PTMI_MK_SMALL_WPC applies: 16 M covers the
+// 4-rank tile shard (10.2 M samples per 64-spp call: +0.7 % over the full
+// grid) and leaves 2-rank shards (20.5 M) and whole frames on the full grid
+// (profiles/r06/ab/mk_small_grid.log).
+#define PTMI_MK_SMALL_GRID_BATCH 16000000
 #endif
 #ifndef PTMI_MK_TAIL_DIV
 #define PTMI_MK_TAIL_DIV 4  // a fetch takes at most (units left) / (TAIL_DIV * waves) units
@@ -791,7 +799,7 @@ static hipError_t launch_mk_trace(const DevScene& sc, const DevFrame& fr, float*
   wk.by_tiles_x = fast_div((uint32_t)wk.tiles_x);
   // Small batches (an 8-rank tile shard) run on a smaller persistent grid, so
   // the next overlapped call's waves share the chip while this one drains.
-  if ((int64_t)fr.w * fr.n_rows * nb < PTMI_MK_SMALL_BATCH && per_cu > PTMI_MK_SMALL_WPC) per_cu = PTMI_MK_SMALL_WPC;
+  if ((int64_t)fr.w * fr.n_rows * nb < PTMI_MK_SMALL_GRID_BATCH && per_cu > PTMI_MK_SMALL_WPC) per_cu = PTMI_MK_SMALL_WPC;
   int64_t waves = (int64_t)(per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
   const int64_t chunks = wk.nunits;
   if (waves > chunks) waves = chunks;
