@@ -196,3 +196,38 @@ def test_stackless_traversal_at_the_bench_call_shape(preset):
     wins = windows_of(run, 4, seed=5)
     o, _ = oracle_windows(run, wins, S0, 3 * run.sps)
     check_windows(g, o, wins, 3 * run.sps, f'{preset} stackless calls {steps}')
+
+
+@pytest.mark.skipif(os.environ.get('PTMI_FULL_TARGET') != '1',
+                    reason='opt-in (PTMI_FULL_TARGET=1): ~90 s of oracle time per preset on 16 threads')
+@pytest.mark.parametrize('preset', ['c2', 'c3'])
+def test_north_star_target_whole_frame_at_full_spp(preset):
+    """The north star's target itself: vol2_final_scene 800x800 at 1024 spp,
+    bench.py's default sequence (warm-up steps, accumulator cleared, 16 timed
+    64-spp steps), every pixel and every device counter of the timed steps
+    against the oracle over the same 655 M samples. Opt-in because the oracle
+    needs ~90 s per preset; its log is kept in profiles/r06/north_star_full_frame.log."""
+    import torch
+    import bench
+    run = bench_run(preset)
+    a = bench.parse(['--preset', preset])
+    acc = torch.zeros((run.H, run.W, 3), dtype=torch.float32, device='cuda')
+    for k in range(a.warmup):
+        run.step(acc, k)
+    torch.cuda.synchronize()
+    acc.zero_()
+    run.integ.reset_counters()
+    for k in range(a.steps):
+        run.step(acc, a.warmup + k)
+    torch.cuda.synchronize()
+    g = acc.cpu().numpy()
+    gst = run.integ.read_counters()
+    spp = a.steps * run.sps
+    assert spp == 1024
+    o, ost = oracle_windows(run, [(0, 0, run.W, run.H)], run.sample_base(a.warmup), spp)
+    linf, exact = compare(g, o, spp)
+    print(f'{preset} north-star target {run.W}x{run.H} x {spp} spp (samples {run.sample_base(a.warmup)}..'
+          f'{run.sample_base(a.warmup) + spp - 1}): L-inf={linf:.3g} identical={exact:.6f} gpu={gst} oracle={ost}')
+    assert linf <= LINF_TOL and exact >= 0.999
+    assert gst == ost
+    assert gst['paths'] == run.W * run.H * spp
