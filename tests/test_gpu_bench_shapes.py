@@ -200,13 +200,14 @@ def test_stackless_traversal_at_the_bench_call_shape(preset):
 
 @pytest.mark.skipif(os.environ.get('PTMI_FULL_TARGET') != '1',
                     reason='opt-in (PTMI_FULL_TARGET=1): ~90 s of oracle time per preset on 16 threads')
-@pytest.mark.parametrize('preset', ['c2', 'c3'])
-def test_north_star_target_whole_frame_at_full_spp(preset):
-    """The north star's target itself: vol2_final_scene 800x800 at 1024 spp,
-    bench.py's default sequence (warm-up steps, accumulator cleared, 16 timed
-    64-spp steps), every pixel and every device counter of the timed steps
-    against the oracle over the same 655 M samples. Opt-in because the oracle
-    needs ~90 s per preset; its log is kept in profiles/r06/north_star_full_frame.log."""
+@pytest.mark.parametrize('preset,full_spp', [('c2', 1024), ('c3', 1024), ('c4', 512)])
+def test_north_star_target_whole_frame_at_full_spp(preset, full_spp):
+    """The north star's target itself: vol2_final_scene 800x800 at 1024 spp
+    (C2 megakernel, C3 wavefront), and C4's 1024x1024 at 512 spp: bench.py's
+    default sequence (warm-up steps, accumulator cleared, 16 timed steps),
+    every pixel and every device counter of the timed steps against the oracle
+    over the same 655 M (537 M) samples. Opt-in because the oracle needs
+    ~90-110 s per preset; its log is kept in profiles/r06/north_star_full_frame.log."""
     import torch
     import bench
     run = bench_run(preset)
@@ -223,10 +224,10 @@ def test_north_star_target_whole_frame_at_full_spp(preset):
     g = acc.cpu().numpy()
     gst = run.integ.read_counters()
     spp = a.steps * run.sps
-    assert spp == 1024
+    assert spp == full_spp
     o, ost = oracle_windows(run, [(0, 0, run.W, run.H)], run.sample_base(a.warmup), spp)
     linf, exact = compare(g, o, spp)
-    print(f'{preset} north-star target {run.W}x{run.H} x {spp} spp (samples {run.sample_base(a.warmup)}..'
+    print(f'{preset} full-spp target {run.W}x{run.H} x {spp} spp (samples {run.sample_base(a.warmup)}..'
           f'{run.sample_base(a.warmup) + spp - 1}): L-inf={linf:.3g} identical={exact:.6f} gpu={gst} oracle={ost}')
     assert linf <= LINF_TOL and exact >= 0.999
     assert gst == ost
