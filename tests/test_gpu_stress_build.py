@@ -47,3 +47,15 @@ def test_stress_build_wavefront_tail_windows(tmp_path):
     assert len(cases) >= 18 and {r['drain_at'] for r in cases} == {16, 1}
     bad = [(r['drain_at'], r['case'], r['n_bad'], r['linf']) for r in cases if r['n_bad'] or r['gpu'] != r['oracle']]
     assert not bad, bad
+
+
+def test_stress_build_whole_frame_bench_calls():
+    """One bench call over the whole frame (tests/test_gpu_bench_shapes.py: C2
+    and C4 megakernel, C3 wavefront; 40.96 M, 33.6 M and 40.96 M paths) with
+    every kernel spilling: every pixel and every device counter equal to the
+    oracle's, as with the shipped build."""
+    p = subprocess.run([sys.executable, '-m', 'pytest', os.path.join(ROOT, 'tests', 'test_gpu_bench_shapes.py'), '-q', '-x',
+                        '-p', 'no:cacheprovider', '-k', 'one_bench_call_full_frame and (c2 or c3 or c4)'],
+                       env=_env(), capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
+    assert '3 passed' in p.stdout, p.stdout[-2000:]
